@@ -1,0 +1,235 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE's own
+code (MVS2.py, HarrisFeatures.py, utils.py at /root/reference) in this
+container, with the OpenCV / pyntcloud stand-ins of tests/golden/standins/.
+
+Run here only (the reference never travels to the GPU box):
+    PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/gen_golden.py [--stage CAP ...]
+
+Outputs (all data, no reference source):
+  seeds_dino.npz        synthetic 2-view SfM tracks (make_seeds.py recipe)
+  func_golden.npz       getDescFeatures+ctNcc pairs, projectPoint, photo tests,
+                        ray_plane_intersection / is_patch_neighbor samples
+  stage_cap{N}.npz      DensePointsWithMVS2 outputs (initial_patches,
+                        all_patches rows) on dinoRing + seeds, queue capped at N pops
+"""
+import argparse
+import contextlib
+import io
+import os
+import queue as _queue
+import sys
+import time
+
+sys.dont_write_bytecode = True
+os.environ.setdefault("MPLBACKEND", "Agg")
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(HERE, "standins"))
+sys.path.insert(1, REF)
+sys.path.insert(2, REPO)
+sys.path.insert(3, HERE)
+
+import numpy as np  # noqa: E402
+
+from make_seeds import load_dino, make_seeds  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+DATA = os.path.join(REPO, "data", "dinoRing")
+PAR = os.path.join(DATA, "dinoR_par.txt")
+
+
+class Args:
+    par_path = PAR
+    scale = 10.0
+    cell_size = 2
+    desc_wid = 5
+    debug = False
+
+
+class Track:
+    def __init__(self, obs):
+        self.point2d_list = obs
+
+
+class SeedSet:
+    """Stands in for GlobalSet: getInfo() -> (n_obs, n_pts, tracks) (GlobalSet.py:36-50)."""
+
+    def __init__(self, tracks):
+        self.tracks = tracks
+
+    def getInfo(self):
+        return 0, len(self.tracks), self.tracks
+
+
+def seeds_to_tracks(seeds):
+    off, view, xy = seeds["track_off"], seeds["obs_view"], seeds["obs_xy"].astype(np.float32)
+    tracks = []
+    for k in range(len(off) - 1):
+        tracks.append(Track([(int(view[o]), xy[o, 0], xy[o, 1]) for o in range(off[k], off[k + 1])]))
+    return tracks
+
+
+def import_reference():
+    import MVS2  # the reference module, unmodified
+    return MVS2
+
+
+def func_golden(MVS2, imgs, K, Rm, t, rng):
+    import HarrisFeatures
+    import utils
+    out = {}
+    V = len(imgs)
+    H, W = imgs[0].shape[:2]
+    gray = [np.asarray(sys.modules["cv2"].cvtColor(im, 6)) for im in imgs]
+    # --- window + ctNcc pairs (HarrisFeatures.py:116-133, MVS2.py:39-43) ---
+    for wid in (5, 3):
+        A, B, S = [], [], []
+        n = 3000
+        while len(S) < n:
+            v1, v2 = rng.integers(0, V, 2)
+            y = rng.uniform(wid, H - wid - 1)
+            x = rng.uniform(wid + 1, W - wid - 1)
+            if len(S) % 3 == 0:   # near the object: mostly textured windows
+                y = rng.uniform(120, 400)
+                x = rng.uniform(150, 500)
+            da = HarrisFeatures.getDescFeatures(imgs[v1], np.array([[y, x]]), wid=wid)[0]
+            db = HarrisFeatures.getDescFeatures(imgs[v2], np.array([[y, x]]), wid=wid)[0]
+            if da is None or db is None:
+                continue
+            with np.errstate(all="ignore"):
+                s = MVS2.ctNcc(da, db)
+            A.append(da); B.append(db); S.append(s)
+        # synthetic windows: random, near-constant, constant, near-threshold pairs
+        npx = (2 * wid + 1) ** 2
+        for k in range(600):
+            kind = k % 4
+            if kind == 0:
+                a = rng.integers(0, 256, npx, dtype=np.uint8); b = rng.integers(0, 256, npx, dtype=np.uint8)
+            elif kind == 1:
+                a = np.full(npx, rng.integers(0, 256), np.uint8); b = rng.integers(0, 256, npx, dtype=np.uint8)
+            elif kind == 2:
+                a = rng.integers(0, 256, npx, dtype=np.uint8)
+                b = np.clip(a.astype(int) + rng.integers(-60, 61, npx), 0, 255).astype(np.uint8)
+            else:
+                a = np.clip(100 + rng.integers(-2, 3, npx), 0, 255).astype(np.uint8)
+                b = np.clip(a.astype(int) + rng.integers(-1, 2, npx), 0, 255).astype(np.uint8)
+            with np.errstate(all="ignore"):
+                s = MVS2.ctNcc(a, b)
+            A.append(a); B.append(b); S.append(s)
+        out[f"ncc_a_w{wid}"] = np.stack(A)
+        out[f"ncc_b_w{wid}"] = np.stack(B)
+        out[f"ncc_s_w{wid}"] = np.array(S, np.float64)
+    # --- window validity edge cases (HarrisFeatures.py:128) ---
+    cases = []
+    for y in (4.9, 5.0, 5.5, H - 7.0, H - 6.5, H - 6.0, -0.5, -1.0):
+        for x in (5.9, 6.0, 6.5, W - 7.0, W - 6.5, W - 6.0, -0.2):
+            d = HarrisFeatures.getDescFeatures(imgs[0], np.array([[y, x]]), wid=5)[0]
+            cases.append((y, x, d is not None))
+    out["desc_edge"] = np.array(cases, np.float64)
+    # --- projectPoint (utils.py:241-244) ---
+    P, C, R_ = [], [], []
+    for k in range(500):
+        v = int(rng.integers(0, V))
+        c = rng.uniform([-0.03, 0.01, -0.03], [0.06, 0.12, 0.06])
+        P.append(utils.projectPoint(c, Rm[v], t[v], K[v])); C.append(c); R_.append(v)
+    out["proj_c"] = np.array(C); out["proj_v"] = np.array(R_, np.int32); out["proj_xy"] = np.array(P)
+    # --- photo_consistenecy_test (MVS2.py:62-77) on bench-distribution candidates ---
+    cs, rs, thrs, Vs, avgs, xys = [], [], [], [], [], []
+    Kinv = [np.linalg.inv(k) for k in K]
+    for k in range(300):
+        v = int(rng.integers(0, V))
+        x = rng.uniform(6, 633) if k % 2 else rng.uniform(150, 500)
+        y = rng.uniform(5, 473) if k % 2 else rng.uniform(100, 420)
+        z = rng.uniform(0.60, 0.72)
+        ray = Kinv[v] @ np.array([x, y, 1.0])
+        c = Rm[v].T @ (z * ray - t[v].ravel())
+        thr = 0.7 if k % 3 else 0.4
+        p = MVS2.MyPatch(c, None, v, None, None, None)
+        with np.errstate(all="ignore"):
+            Vl = p.photo_consistenecy_test(imgs, K, Rm, t, MIN_NCC=thr)
+        cs.append(c); rs.append(v); thrs.append(thr)
+        Vs.append([e[0] for e in Vl]); avgs.append(p.avg_ncc_score)
+        xys.append(utils.projectPoint(c, Rm[v], t[v], K[v]))
+    out["pt_c"] = np.array(cs); out["pt_R"] = np.array(rs, np.int32); out["pt_thr"] = np.array(thrs)
+    words = (V + 63) // 64
+    mask = np.zeros((len(Vs), words), np.uint64)
+    for i, vl in enumerate(Vs):
+        for e in vl:
+            mask[i, e // 64] |= np.uint64(1) << np.uint64(e % 64)
+    out["pt_mask"] = mask
+    out["pt_count"] = np.array([len(v) for v in Vs], np.int32)
+    out["pt_avg"] = np.array(avgs, np.float64)
+    out["pt_xy"] = np.array(xys)
+    # --- ray_plane_intersection / is_patch_neighbor (MVS2.py:298-306) ---
+    rp = []
+    for k in range(500):
+        o = rng.normal(size=3); d = rng.normal(size=3); d /= np.linalg.norm(d)
+        pc = rng.normal(size=3); pn = rng.normal(size=3); pn /= np.linalg.norm(pn)
+        X = MVS2.ray_plane_intersection(o, d, pc, pn)
+        a = MVS2.MyPatch(pc, pn, 0, None, None, None)
+        xn = rng.normal(size=3); xn /= np.linalg.norm(xn)
+        b = MVS2.MyPatch(X, xn, 0, None, None, None)
+        nb = MVS2.is_patch_neighbor(a, b, threshold=0.1)
+        rp.append(np.concatenate([o, d, pc, pn, X, xn, [float(nb)]]))
+    out["rayplane"] = np.array(rp)
+    return out
+
+
+def stage_golden(MVS2, imgs, tracks, cap):
+    import pyntcloud
+
+    class CappedQueue(_queue.Queue):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            self.gets = 0
+
+        def get(self, *a, **k):
+            self.gets += 1
+            return super().get(*a, **k)
+
+        def empty(self):
+            return self.gets >= cap or super().empty()
+
+    MVS2.queue.Queue = CappedQueue
+    pyntcloud.written.clear()
+    t0 = time.time()
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf), np.errstate(all="ignore"):
+        MVS2.DensePointsWithMVS2(imgs, SeedSet(tracks), Args())
+    dt = time.time() - t0
+    ntests = buf.getvalue().count("iteration:")
+    return {"initial_patches": pyntcloud.written["initial_patches.ply"],
+            "all_patches": pyntcloud.written["all_patches.ply"],
+            "cap": np.int64(cap), "ref_seconds": np.float64(dt), "pops": np.int64(ntests)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--func", action="store_true")
+    ap.add_argument("--seeds", action="store_true")
+    ap.add_argument("--stage", type=int, nargs="*", default=[])
+    a = ap.parse_args()
+    assert os.path.isdir(REF), "the reference is only present in the build container"
+    imgs, K, Rm, t = load_dino(DATA)
+    if a.seeds or not os.path.exists(os.path.join(HERE, "seeds_dino.npz")):
+        seeds = make_seeds(imgs, K, Rm, t)
+        np.savez_compressed(os.path.join(HERE, "seeds_dino.npz"), **seeds)
+        print("seeds:", len(seeds["track_off"]) - 1, "tracks")
+    seeds = dict(np.load(os.path.join(HERE, "seeds_dino.npz")))
+    MVS2 = import_reference()
+    if a.func:
+        rng = np.random.default_rng(12345)
+        out = func_golden(MVS2, imgs, K, Rm, t, rng)
+        np.savez_compressed(os.path.join(HERE, "func_golden.npz"), **out)
+        print("func golden written", {k: v.shape for k, v in out.items()})
+    for cap in a.stage:
+        out = stage_golden(MVS2, imgs, seeds_to_tracks(seeds), cap)
+        np.savez_compressed(os.path.join(HERE, f"stage_cap{cap}.npz"), **out)
+        print(f"stage cap {cap}: initial {len(out['initial_patches'])} all {len(out['all_patches'])} "
+              f"in {out['ref_seconds']:.1f}s")
+
+
+if __name__ == "__main__":
+    main()
