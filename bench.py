@@ -1,0 +1,219 @@
+"""Benchmark: candidate patches NCC-scored per second (BASELINE.json metric).
+
+Workload (BASELINE configs[1]): the real dinoRing
+gray stack (48 views x 640x480, data/dinoRing), one expansion sweep = a batch
+of 2^20 synthetic candidate patches per GPU (reference view, sub-pixel pixel,
+depth 0.60-0.72 m; seed 0 + rank), every candidate photo-tested against all 48
+views with the reference's 11x11 window (wid=5, MVS2.py:64/69) at MIN_NCC 0.7.
+A step = score the sweep on the GPU (inputs resident in HBM) + compact the
+accepted candidates (|V| >= 3) + RCCL all-gather of the accepted records
+across ranks (the sweep's exchange step; skipped at N=1).
+
+python bench.py [--gpus N --steps K --warmup W --n CANDS --wid 5]
+N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_NAME = "simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd"
+sys.path.insert(0, REPO)
+
+PEAK_HBM = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(V, wid):
+    """V*(2w+1)^2 window bytes + 32 B in + 8*ceil(V/64) + 16 B out."""
+    return V * (2 * wid + 1) ** 2 + 32 + 8 * ((V + 63) // 64) + 16
+
+
+def load_scene():
+    from PIL import Image
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "data", "dinoRing", "*.png")))
+    rgb = np.stack([np.asarray(Image.open(f).convert("RGB")) for f in files])
+    par = os.path.join(REPO, "data", "dinoRing", "dinoR_par.txt")
+    K, R, t = [], [], []
+    for line in open(par).readlines()[1:]:
+        v = [float(x) for x in line.split()[1:]]
+        K.append(np.array(v[0:9]).reshape(3, 3))
+        R.append(np.array(v[9:18]).reshape(3, 3))
+        t.append(np.array(v[18:21]))
+    return rgb, np.array(K), np.array(R), np.array(t)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1 << 20, help="candidates per GPU per sweep")
+    ap.add_argument("--wid", type=int, default=5)
+    ap.add_argument("--thr", type=float, default=0.7)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=100000)
+    ap.add_argument("--secondary-wid", type=int, default=3)
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    pkg = importlib.import_module(PKG_NAME)
+
+    rgb, K, R, t = load_scene()
+    V = len(rgb)
+    ctx = pkg.MvsContext(rgb, K, R, t, device=local)
+    c_np, ref_np = pkg.synthetic.candidates(a.n, K, R, t, seed=rank)
+    c = torch.from_numpy(c_np).to(dev)
+    ref = torch.from_numpy(ref_np).to(dev)
+    n = a.n
+    words = (V + 63) // 64
+    xy = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    mask = torch.empty((n, words), dtype=torch.int64, device=dev)
+    count = torch.empty(n, dtype=torch.int32, device=dev)
+    avg = torch.empty(n, dtype=torch.float64, device=dev)
+    vlb = 3 if V > 2 else 2
+    stream = torch.cuda.current_stream(dev)
+    gathered = {"n": 0}
+
+    def step(wid, evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        ctx.score_device(c, ref, xy, mask, count, avg, a.thr, wid, stream=stream.cuda_stream)
+        if evs is not None:
+            evs[1].record(stream)
+        if world > 1:
+            # the sweep's exchange: accepted records (index, count, mask, xy) to every rank
+            acc = torch.nonzero(count >= vlb).squeeze(1)
+            k = torch.tensor([acc.numel()], device=dev, dtype=torch.int64)
+            ks = [torch.empty_like(k) for _ in range(world)]
+            dist.all_gather(ks, k)
+            kmax = max(int(x.item()) for x in ks)
+            recw = 2 + words + 2
+            buf = torch.zeros((max(kmax, 1), recw), dtype=torch.int64, device=dev)
+            m = acc.numel()
+            if m:
+                buf[:m, 0] = acc
+                buf[:m, 1] = count[acc].to(torch.int64)
+                buf[:m, 2:2 + words] = mask[acc]
+                buf[:m, 2 + words:] = xy[acc].view(torch.int64)
+            out = torch.empty((world * buf.shape[0], recw), dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(out, buf)
+            gathered["n"] = sum(int(x.item()) for x in ks)
+
+    def timed(wid, steps, warmup):
+        for _ in range(warmup):
+            step(wid)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(wid, evs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        kms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / steps   # score kernel, HIP events
+        if world > 1:
+            tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        return dt, kms
+
+    dt, kms = timed(a.wid, a.steps, a.warmup)
+    total = n * world * a.steps
+    value = total / dt
+    B = algorithmic_bytes(V, a.wid)
+    achieved = B * n / (kms * 1e-3)
+    accepted = int((count >= vlb).sum().item())
+    sec = None
+    if a.secondary_wid and a.secondary_wid != a.wid:
+        dt2, kms2 = timed(a.secondary_wid, max(a.steps // 2, 5), 2)
+        B2 = algorithmic_bytes(V, a.secondary_wid)
+        sec = {"wid": a.secondary_wid, "value": n * world * max(a.steps // 2, 5) / dt2,
+               "kernel_ms": kms2, "achieved_GBps": B2 * n / (kms2 * 1e-3) / 1e9}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO))
+        from oracle import oracle as orc
+        scene = orc.Scene(rgb, K, R, t)
+        m = min(a.cpu_sample, n)
+        t0 = time.perf_counter()
+        oxy, omask, ocount, _ = scene.score_batch(c_np[:m], ref_np[:m], a.thr, a.wid, nthreads=1)
+        cdt = time.perf_counter() - t0
+        # the sample doubles as a parity spot check of the measured launch
+        step(a.wid)
+        torch.cuda.synchronize()
+        cnt_gpu = count[:m].cpu().numpy()
+        cpu = {"value": m / cdt, "unit": "candidates/s", "cores": 1, "kind": "port",
+               "sample": f"first {m} of the rank-0 sweep (same candidates, wid={a.wid}), "
+                         f"oracle/mvs_oracle.c or_score_batch single-threaded, {cdt:.1f} s",
+               "parity_on_sample": bool(np.array_equal(cnt_gpu, ocount) and
+                                        np.array_equal(mask[:m].cpu().numpy().view(np.uint64), omask))}
+        if not cpu["parity_on_sample"]:
+            print("WARNING: GPU/oracle mismatch on the cpu-baseline sample", file=sys.stderr)
+
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get("n") == n and tj.get("wid") == a.wid and tj.get("V") == V:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "candidate patches/sec NCC-scored (640×480, 48 views) at 1/2/4/8 MI355X; % HBM roofline",
+            "value": value,
+            "unit": "candidates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "real dinoRing images (data/dinoRing) + synthetic candidate patches (seed = rank)",
+            "config": {"workload": f"dinoRing 48x640x480, one expansion sweep of {n} candidates per GPU, "
+                                   f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
+                                   f"MIN_NCC {a.thr}, accepted records all-gathered",
+                       "global_batch": n * world, "wid": a.wid, "views": V,
+                       "parallelism": f"candidate-queue shards x{world} (RCCL all-gather)"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM,
+                         "traffic": traffic,
+                         "kernel": "k_score<5,1>" if a.wid == 5 else f"k_score<{a.wid},1>",
+                         "kernel_ms": kms, "bytes_per_candidate": B},
+            "cpu_baseline": cpu,
+            "accepted_per_sweep": accepted,
+            "gathered_records": gathered["n"],
+            "secondary": sec,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

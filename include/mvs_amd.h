@@ -1,0 +1,114 @@
+/*
+ * mvs_amd.h -- C-ABI of the MI355X-native MVS patch-expansion library
+ * (libmvs_amd.so, built from
+ *  simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd/csrc).
+ *
+ * The reference (MarvinChung/simple-implementation-of-structure-from-motion-
+ * and-multi-view-stereo-by-python) is pure Python with no FFI; each entry point
+ * below names the Python interface it replaces.  Conventions:
+ *   - plain pointers and sizes, no torch / C++ types;
+ *   - every call returns 0 on success or a negative status
+ *     (MVS_E_ARG, MVS_E_HIP, MVS_E_UNSUPPORTED, MVS_E_NOMEM); the message is in
+ *     mvs_last_error(ctx) (or mvs_last_error(NULL) when create failed);
+ *   - no C++ exception crosses the ABI;
+ *   - one context per device, driven by one host thread; *_device calls are
+ *     ordered on the caller's HIP stream (NULL = the context's stream).
+ *
+ * Arrays follow the reference's numpy conventions: K/R row-major 3x3 per view
+ * (V*9 doubles), t 3 per view, images V*H*W*3 uint8 RGB (main.py:17-18), view
+ * index = position in the sorted image list = par-file row - 1 (utils.py:72-80).
+ */
+#ifndef MVS_AMD_H
+#define MVS_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVS_OK 0
+#define MVS_E_ARG (-1)
+#define MVS_E_HIP (-2)
+#define MVS_E_UNSUPPORTED (-3)
+#define MVS_E_NOMEM (-4)
+
+typedef struct mvs_ctx mvs_ctx;
+typedef struct mvs_stage_result mvs_stage_result;
+
+/* Library version string. */
+const char* mvs_version(void);
+
+/* Scene setup: replaces the per-call work the reference redoes on every photo
+ * test -- read_pars (utils.py:56-81, called at MVS2.py:178/309), the per-call
+ * full-frame copy + cvtColor(BGR2GRAY) (HarrisFeatures.py:124-125) and
+ * cv2.Rodrigues(par_r) (utils.py:242).  Uploads the images once, builds the
+ * device gray stack (OpenCV BGR2GRAY fixed-point formula applied to the RGB
+ * data, as the reference does) and the per-view camera table.
+ * Rp may be NULL (the library computes R' = Rodrigues(Rodrigues(R))).
+ * V <= 256, H, W >= 16. */
+int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const double* K,
+                   const double* R, const double* t, const double* Rp, mvs_ctx** out);
+void mvs_ctx_destroy(mvs_ctx* ctx);
+const char* mvs_last_error(const mvs_ctx* ctx);
+/* Copies the rotations the projection uses (V*9) -- for parity tests. */
+int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp);
+
+/* Batched MyPatch.photo_consistenecy_test (MVS2.py:62-77): for candidate i
+ * with centre c[3i..3i+2] and reference view ref[i], project into ref[i]
+ * (projectPoint, utils.py:241-244), take the (2*wid+1)^2 windows of every view
+ * at that pixel (getDescFeatures, HarrisFeatures.py:116-133; all views at the
+ * reference view's pixel, MVS2.py:68), and keep the views idx != ref with
+ * ctNcc > min_ncc (MVS2.py:39-43, 72).
+ * Outputs: xy[2i..] = projection (the x, y of every V entry, MVS2.py:74);
+ * mask[i*words + w] bit b = view 64w+b passed (words = ceil(V/64));
+ * count[i] = |V|; avg[i] = mean ncc of the passing views (avg_ncc_score).
+ * Host pointers; synchronous. wid in 1..5. */
+int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int wid,
+              double min_ncc, double* xy, uint64_t* mask, int32_t* count, double* avg);
+/* Same on device pointers (e.g. torch tensor data_ptr()), stream-ordered. */
+int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
+                     double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
+                     double* d_avg, void* stream);
+/* Number of per-view NCC decisions that fell within 1e-9 of the threshold
+ * and were re-evaluated in numpy order since the context was created. */
+int64_t mvs_exact_hits(mvs_ctx* ctx);
+
+/* ctNcc (MVS2.py:39-43) on n explicit window pairs of npx (<= 128) uint8
+ * pixels each (device pointers).  ncc[i] = closed-form value (numpy-order
+ * value if force_exact or within 1e-9 of thr; nan for a constant window);
+ * pass[i] = ncc > thr. */
+int mvs_ncc_windows(int64_t n, int npx, const uint8_t* d_a, const uint8_t* d_b, double thr,
+                    int force_exact, double* d_ncc, uint8_t* d_pass, void* stream);
+
+/* DensePointsWithMVS2 (MVS2.py:176-295) without file IO: seeding from the SfM
+ * tracks (MVS2.py:205-260), patch_expansion (MVS2.py:308-404, FIFO capped at
+ * min(max_pops, 100000) pops) and reconstruct_from_Q ordering
+ * (MVS2.py:159-173).  Tracks: track t owns observations
+ * [track_off[t], track_off[t+1]); obs_view = image index, obs_xy = (x, y)
+ * float32 pairs (GlobalSet point2d_list); element 0 is the reference view.
+ * cell_size / scale / wid as args.cell_size, args.scale and the photo test's
+ * window half-width (5 in the reference). */
+int mvs_stage_run(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off,
+                  const int32_t* obs_view, const float* obs_xy, int cell_size, double scale,
+                  int wid, int64_t max_pops, mvs_stage_result** out);
+/* which = 0: initial_patches rows, 1: all_patches rows (x,y,z,r,g,b float64). */
+int64_t mvs_stage_count(const mvs_stage_result* res, int which);
+int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows);
+/* stats[0..7] = pops, reference-equivalent photo tests, accepted patches,
+ * queue entries left, candidates scored on the GPU, sweeps, seed candidates,
+ * exact-path decisions. */
+int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats);
+void mvs_stage_free(mvs_stage_result* res);
+
+/* Host geometry the stage uses, exported for parity tests:
+ * cv2.Rodrigues round trip (utils.py:242-243) and cv2.triangulatePoints for one
+ * point (utils.py:238-239, homogeneous 4-vector). */
+int mvs_rodrigues_roundtrip(const double* R, double* Rp);
+int mvs_triangulate(const double* P1, const double* P2, const double* x1, const double* x2,
+                    double* X4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVS_AMD_H */

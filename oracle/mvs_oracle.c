@@ -26,6 +26,7 @@
  *   cv2.triangulatePoints         -> or_triangulate        (utils.py:239)
  *   cv::JacobiSVD (used by both)  -> or_jacobi_svd
  */
+#define _GNU_SOURCE
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -168,7 +169,12 @@ void or_rodrigues_v2m(const double *rv, double *R) {
         for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
         return;
     }
-    double c = cos(theta), s = sin(theta), c1 = 1. - c;
+    /* glibc sincos(): what gcc emits for OpenCV's adjacent cos/sin calls at
+     * -O2 (it differs from separate sin()/cos() in the last bit for some
+     * arguments); called explicitly so every build agrees. */
+    double c, s;
+    sincos(theta, &s, &c);
+    double c1 = 1. - c;
     double itheta = theta ? 1. / theta : 0.;
     rx *= itheta; ry *= itheta; rz *= itheta;
     double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};

@@ -1,0 +1,103 @@
+"""Drop-in for the reference's MVS stage (MVS2.py), running on MI355X.
+
+DensePointsWithMVS2(imgs, global_set, args)   MVS2.py:176-295
+    Same arguments, prints and side effects (initial_patches.ply,
+    all_patches.ply in the working directory).  Seeding, the 100k-pop FIFO
+    expansion and the cell-table output order run in libmvs_amd.so: photo
+    tests on the GPU (HIP, gfx950), the order-dependent commit on the host.
+MyPatch.photo_consistenecy_test(...)          MVS2.py:62-77
+    Same method on the same fields; one-candidate call of the batched GPU
+    scorer.  Use photo_consistency_batch for many candidates.
+"""
+import time
+
+import numpy as np
+
+from . import _lib
+from .utils import export2ply, pars_to_arrays, read_pars, tracks_to_arrays
+
+last_stats = {}
+_ctx_cache = {}
+
+
+def _device_index():
+    import os
+    return int(os.environ.get("LOCAL_RANK", os.environ.get("MVS_DEVICE", "0")))
+
+
+def scene_context(imgs, par_K, par_r, par_t, device=None):
+    """MvsContext for (imgs, cameras), cached on the identity of imgs."""
+    key = (id(imgs), len(imgs), id(par_K), id(par_r), id(par_t))
+    ctx = _ctx_cache.get(key)
+    if ctx is None:
+        K, R, t = pars_to_arrays(par_K, par_r, par_t, len(imgs))
+        ctx = _lib.MvsContext(imgs, K, R, t, device=_device_index() if device is None else device)
+        _ctx_cache.clear()
+        _ctx_cache[key] = (ctx, imgs)
+        return ctx
+    return ctx[0]
+
+
+class MyPatch(object):
+    """Patch record with the reference's fields (MVS2.py:45-57)."""
+
+    def __init__(self, centroid, normal, reference_img_index, visible_set, color, dist, patch_size=5):
+        self.dist = dist
+        self.c = centroid
+        self.n = normal
+        self.R = reference_img_index
+        self.V = visible_set if visible_set is not None else []
+        self.color = color
+        self.patch_size = patch_size
+        self.avg_ncc_score = 0
+
+    def visible_ct(self):
+        return len(self.V)
+
+    def photo_consistenecy_test(self, imgs, par_K, par_r, par_t, MIN_NCC=0.7):
+        ctx = scene_context(imgs, par_K, par_r, par_t)
+        xy, mask, count, avg = ctx.score(np.asarray(self.c, np.float64)[None], [self.R], MIN_NCC, 5)
+        for idx in _mask_views(mask[0]):
+            self.V.append([idx, xy[0, 0], xy[0, 1]])
+        self.avg_ncc_score = float(avg[0])
+        return self.V
+
+
+def _mask_views(words):
+    out = []
+    for w, m in enumerate(np.asarray(words, np.uint64)):
+        m = int(m)
+        while m:
+            b = (m & -m).bit_length() - 1
+            out.append(64 * w + b)
+            m &= m - 1
+    return out
+
+
+def photo_consistency_batch(ctx, centroids, ref_views, MIN_NCC=0.7, wid=5):
+    """Batched photo test: (xy, mask, count, avg) per candidate."""
+    return ctx.score(centroids, ref_views, MIN_NCC, wid)
+
+
+def DensePointsWithMVS2(imgs, global_set, args, max_pops=100000, device=None):
+    """MVS2.py:176-295 on the GPU.  Returns None like the reference; the run's
+    counters are left in MVS2.last_stats."""
+    t0 = time.time()
+    par_K, par_r, par_t = read_pars(args)
+    n_observations, n_world_points, legal_sets = global_set.getInfo()
+    track_off, obs_view, obs_xy = tracks_to_arrays(legal_sets)
+    ctx = scene_context(imgs, par_K, par_r, par_t, device)
+    initial, allp, stats = ctx.stage(track_off, obs_view, obs_xy, cell_size=args.cell_size,
+                                     scale=args.scale, wid=5, max_pops=max_pops)
+    print("len of initial patches", len(initial))
+    export2ply(initial[:, :3], initial[:, 3:], path="initial_patches")
+    print("filter outliers")
+    print("reconstruct point cloud")
+    t1 = time.time()
+    print("Optimization took {0:.0f} seconds".format(t1 - t0))
+    print("points len:", len(allp))
+    export2ply(allp[:, :3], allp[:, 3:], path="all_patches")
+    stats["seconds"] = t1 - t0
+    last_stats.clear()
+    last_stats.update(stats)
+    return None

@@ -1,0 +1,230 @@
+"""ctypes binding of libmvs_amd.so (include/mvs_amd.h).
+
+The product path has no CPU fallback: if the HIP library is missing or fails
+to load, every entry point raises RuntimeError (the one exception the
+reference's main() catches, main.py:43-46).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmvs_amd.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_fp = ctypes.POINTER(ctypes.c_float)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+
+# (name, restype, argtypes) -- mirrors include/mvs_amd.h one to one
+SIGNATURES = [
+    ("mvs_version", ctypes.c_char_p, []),
+    ("mvs_last_error", ctypes.c_char_p, [_vp]),
+    ("mvs_ctx_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p,
+                                      _dp, _dp, _dp, _dp, ctypes.POINTER(_vp)]),
+    ("mvs_ctx_destroy", None, [_vp]),
+    ("mvs_ctx_rproj", ctypes.c_int, [_vp, _dp]),
+    ("mvs_score", ctypes.c_int, [_vp, ctypes.c_int64, _dp, _i32p, ctypes.c_int, ctypes.c_double,
+                                 _dp, _u64p, _i32p, _dp]),
+    ("mvs_score_device", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int,
+                                        ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
+    ("mvs_exact_hits", ctypes.c_int64, [_vp]),
+    ("mvs_ncc_windows", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_double,
+                                       ctypes.c_int, _vp, _vp, _vp]),
+    ("mvs_stage_run", ctypes.c_int, [_vp, ctypes.c_int64, _i64p, _i32p, _fp, ctypes.c_int,
+                                     ctypes.c_double, ctypes.c_int, ctypes.c_int64,
+                                     ctypes.POINTER(_vp)]),
+    ("mvs_stage_count", ctypes.c_int64, [_vp, ctypes.c_int]),
+    ("mvs_stage_rows", ctypes.c_int, [_vp, ctypes.c_int, _dp]),
+    ("mvs_stage_stats", ctypes.c_int, [_vp, _i64p]),
+    ("mvs_stage_free", None, [_vp]),
+    ("mvs_rodrigues_roundtrip", ctypes.c_int, [_dp, _dp]),
+    ("mvs_triangulate", ctypes.c_int, [_dp, _dp, _dp, _dp, _dp]),
+]
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libmvs_amd.so; raises RuntimeError if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libmvs_amd.so not found at {path}: build it with __graft_entry__.build() "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:
+        raise RuntimeError(f"cannot load {path}: {e}") from e
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def last_error(ctx=None):
+    msg = load().mvs_last_error(ctx)
+    return msg.decode() if msg else ""
+
+
+def check(rc, ctx=None, what="mvs"):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error(ctx)}")
+
+
+def rodrigues_roundtrip(R):
+    """R' = Rodrigues(Rodrigues(R)) -- the rotation cv2.projectPoints applies (utils.py:242-243)."""
+    R = _c(R, np.float64).reshape(9)
+    out = np.empty(9)
+    check(load().mvs_rodrigues_roundtrip(_p(R, _dp), _p(out, _dp)), what="rodrigues")
+    return out.reshape(3, 3)
+
+
+def triangulate(P1, P2, x1, x2):
+    """cv2.triangulatePoints for one correspondence (utils.py:238-239), homogeneous 4-vector."""
+    P1 = _c(P1, np.float64).reshape(12)
+    P2 = _c(P2, np.float64).reshape(12)
+    x1 = _c(x1, np.float64).reshape(2)
+    x2 = _c(x2, np.float64).reshape(2)
+    out = np.empty(4)
+    check(load().mvs_triangulate(_p(P1, _dp), _p(P2, _dp), _p(x1, _dp), _p(x2, _dp), _p(out, _dp)),
+          what="triangulate")
+    return out
+
+
+class MvsContext:
+    """One device-resident scene (images + cameras) on one GPU.
+
+    imgs: (V,H,W,3) uint8 RGB (main.py:17-18 convention) or a list of such
+    frames; K, R: (V,3,3); t: (V,3) or (V,3,1).
+    """
+
+    def __init__(self, imgs, K, R, t, device=0, Rp=None):
+        lib = load()
+        rgb = _c(np.stack(imgs) if isinstance(imgs, (list, tuple)) else imgs, np.uint8)
+        if rgb.ndim != 4 or rgb.shape[-1] != 3:
+            raise RuntimeError(f"images must be (V,H,W,3) uint8 RGB, got {rgb.shape}")
+        self.V, self.H, self.W = (int(x) for x in rgb.shape[:3])
+        self.words = (self.V + 63) // 64
+        K = _c(K, np.float64).reshape(self.V, 9)
+        R = _c(R, np.float64).reshape(self.V, 9)
+        t = _c(t, np.float64).reshape(self.V, 3)
+        rp = _c(Rp, np.float64).reshape(self.V, 9) if Rp is not None else None
+        h = _vp()
+        rc = lib.mvs_ctx_create(int(device), self.V, self.H, self.W, _p(rgb, _u8p), _p(K, _dp),
+                                _p(R, _dp), _p(t, _dp), _p(rp, _dp) if rp is not None else None,
+                                ctypes.byref(h))
+        check(rc, None, "mvs_ctx_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().mvs_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def rproj(self):
+        out = np.empty((self.V, 9))
+        check(load().mvs_ctx_rproj(self._h, _p(out, _dp)), self._h, "mvs_ctx_rproj")
+        return out.reshape(self.V, 3, 3)
+
+    def exact_hits(self):
+        return int(load().mvs_exact_hits(self._h))
+
+    def score(self, c, ref, min_ncc=0.7, wid=5):
+        """Batched photo_consistenecy_test (MVS2.py:62-77) on host arrays.
+
+        Returns xy (n,2), mask (n,words) uint64, count (n,), avg (n,)."""
+        c = _c(c, np.float64).reshape(-1, 3)
+        ref = _c(ref, np.int32).reshape(-1)
+        n = len(ref)
+        if len(c) != n:
+            raise RuntimeError("c and ref lengths differ")
+        xy = np.empty((n, 2))
+        mask = np.empty((n, self.words), np.uint64)
+        count = np.empty(n, np.int32)
+        avg = np.empty(n)
+        rc = load().mvs_score(self._h, n, _p(c, _dp), _p(ref, _i32p), int(wid), float(min_ncc),
+                              _p(xy, _dp), _p(mask, _u64p), _p(count, _i32p), _p(avg, _dp))
+        check(rc, self._h, "mvs_score")
+        return xy, mask, count, avg
+
+    def score_device(self, c, ref, xy, mask, count, avg, min_ncc=0.7, wid=5, stream=None):
+        """Same on device tensors (torch: pass .data_ptr() ints); stream-ordered."""
+        n = int(ref.numel()) if hasattr(ref, "numel") else int(len(ref))
+        ptr = (lambda x: x.data_ptr()) if hasattr(ref, "data_ptr") else (lambda x: int(x))
+        rc = load().mvs_score_device(self._h, n, ptr(c), ptr(ref), int(wid), float(min_ncc),
+                                     ptr(xy), ptr(mask), ptr(count), ptr(avg),
+                                     stream if stream is not None else None)
+        check(rc, self._h, "mvs_score_device")
+
+    def stage(self, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5, max_pops=100000):
+        """DensePointsWithMVS2 minus IO; returns (initial N0x6, all Nx6, stats dict)."""
+        lib = load()
+        track_off = _c(track_off, np.int64)
+        obs_view = _c(obs_view, np.int32)
+        obs_xy = _c(obs_xy, np.float32).reshape(-1, 2)
+        res = _vp()
+        rc = lib.mvs_stage_run(self._h, len(track_off) - 1, _p(track_off, _i64p),
+                               _p(obs_view, _i32p), _p(obs_xy, _fp), int(cell_size), float(scale),
+                               int(wid), int(max_pops), ctypes.byref(res))
+        check(rc, self._h, "mvs_stage_run")
+        try:
+            out = []
+            for which in (0, 1):
+                n = lib.mvs_stage_count(res, which)
+                rows = np.empty((n, 6))
+                if n:
+                    check(lib.mvs_stage_rows(res, which, _p(rows, _dp)), self._h, "mvs_stage_rows")
+                out.append(rows)
+            st = np.empty(8, np.int64)
+            check(lib.mvs_stage_stats(res, _p(st, _i64p)), self._h, "mvs_stage_stats")
+        finally:
+            lib.mvs_stage_free(res)
+        keys = ["pops", "tests", "accepts", "queue_left", "scored", "sweeps", "seed_candidates",
+                "exact_hits"]
+        return out[0], out[1], dict(zip(keys, (int(x) for x in st)))
+
+
+def ncc_windows(a, b, thr, force_exact=False, stream=None):
+    """ctNcc on device window pairs (torch uint8 tensors (n, npx)); returns (ncc, pass) tensors."""
+    import torch
+    n, npx = a.shape
+    ncc = torch.empty(n, dtype=torch.float64, device=a.device)
+    ok = torch.empty(n, dtype=torch.uint8, device=a.device)
+    rc = load().mvs_ncc_windows(n, npx, a.data_ptr(), b.data_ptr(), float(thr), int(force_exact),
+                                ncc.data_ptr(), ok.data_ptr(), stream)
+    check(rc, None, "mvs_ncc_windows")
+    return ncc, ok

@@ -1,0 +1,41 @@
+"""Build recipe for libmvs_amd.so (hipcc, gfx950).  Used by __graft_entry__.build().
+
+-ffp-contract=off on both host and device code: the photo test's geometry
+reproduces the reference's binary64 operation order; the only fused products
+are the ones written as fma() (numpy/OpenBLAS 3-element dot products).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libmvs_amd.so")
+SOURCES = ["mvs_kernels.hip", "mvs_engine.cpp"]
+HEADERS = ["mvs_internal.h", os.path.join("..", "..", "include", "mvs_amd.h")]
+ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
+
+
+def needs_build():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
+
+
+def build(force=False, verbose=False):
+    if not force and not needs_build():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+           "-o", LIB + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd, cwd=CSRC)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

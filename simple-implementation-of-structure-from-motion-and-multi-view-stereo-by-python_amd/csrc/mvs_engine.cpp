@@ -1,0 +1,932 @@
+// Host side of libmvs_amd.so: scene context, camera table, seeding, the
+// ordered expansion commit engine and the C-ABI of include/mvs_amd.h.
+//
+// Reference: MVS2.py:176-404 (DensePointsWithMVS2, patch_expansion,
+// CellTable), utils.py:234-254 (geometry helpers).
+//
+// Design.  Everything a candidate's photo test and accept test depend on is
+// immutable (parent patch, cameras, images), so scoring runs speculatively on
+// the GPU in sweeps; only the cell-table vacancy checks, the FIFO order, the
+// `break` of the j loop and the pop cap are order dependent, and those are
+// replayed here on the host exactly in reference order.  A patch's children
+// -- (hit view, i in {-1,+1}); the geometry does not depend on j
+// (MVS2.py:334) -- are scored once per distinct record and memoised.
+//
+// Compiled with -ffp-contract=off: host geometry (Jacobi SVD, triangulation,
+// camera constants) follows OpenCV's / numpy's operation order.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mvs_amd.h"
+#include "mvs_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Fail {
+    int code;
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                         \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess)                                                             \
+            throw Fail{MVS_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)};        \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        release();
+        if (count == 0) count = 1;
+        HIPCHK(hipMalloc((void**)&p, count * sizeof(T)));
+        n = count;
+    }
+    void ensure(size_t count) {
+        if (count > n) alloc(std::max(count, n * 2));
+    }
+    // grow preserving the first `keep` elements
+    void grow(size_t count, size_t keep, hipStream_t s) {
+        if (count <= n) return;
+        T* q = nullptr;
+        size_t nn = std::max(count, n * 2);
+        HIPCHK(hipMalloc((void**)&q, nn * sizeof(T)));
+        if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        release();
+        p = q;
+        n = nn;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Host geometry (OpenCV 4.x algorithms the reference calls through cv2)
+// ---------------------------------------------------------------------------
+
+// cv::JacobiSVDImpl_<double>: one-sided Jacobi on the n rows (length m) of At.
+void jacobi_svd(double* At, double* Wout, double* Vt, int m, int n) {
+    double W[16];
+    const double eps = DBL_EPSILON * 10, minval = DBL_MIN;
+    const int max_iter = std::max(m, 30);
+    for (int i = 0; i < n; i++) {
+        double sd = 0;
+        for (int k = 0; k < m; k++) {
+            const double t = At[i * m + k];
+            sd += t * t;
+        }
+        W[i] = sd;
+        for (int k = 0; k < n; k++) Vt[i * n + k] = 0;
+        Vt[i * n + i] = 1;
+    }
+    for (int iter = 0; iter < max_iter; iter++) {
+        bool changed = false;
+        for (int i = 0; i < n - 1; i++)
+            for (int j = i + 1; j < n; j++) {
+                double* Ai = At + i * m;
+                double* Aj = At + j * m;
+                double a = W[i], p = 0, b = W[j];
+                for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
+                if (std::fabs(p) <= eps * std::sqrt(a * b)) continue;
+                p *= 2;
+                const double beta = a - b, gamma = std::hypot(p, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = std::sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = std::sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                a = b = 0;
+                for (int k = 0; k < m; k++) {
+                    const double t0 = c * Ai[k] + s * Aj[k];
+                    const double t1 = -s * Ai[k] + c * Aj[k];
+                    Ai[k] = t0;
+                    Aj[k] = t1;
+                    a += t0 * t0;
+                    b += t1 * t1;
+                }
+                W[i] = a;
+                W[j] = b;
+                changed = true;
+                double* Vi = Vt + i * n;
+                double* Vj = Vt + j * n;
+                for (int k = 0; k < n; k++) {
+                    const double t0 = c * Vi[k] + s * Vj[k];
+                    const double t1 = -s * Vi[k] + c * Vj[k];
+                    Vi[k] = t0;
+                    Vj[k] = t1;
+                }
+            }
+        if (!changed) break;
+    }
+    for (int i = 0; i < n; i++) {
+        double sd = 0;
+        for (int k = 0; k < m; k++) {
+            const double t = At[i * m + k];
+            sd += t * t;
+        }
+        W[i] = std::sqrt(sd);
+    }
+    for (int i = 0; i < n - 1; i++) {
+        int j = i;
+        for (int k = i + 1; k < n; k++)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            std::swap(W[i], W[j]);
+            for (int k = 0; k < m; k++) std::swap(At[i * m + k], At[j * m + k]);
+            for (int k = 0; k < n; k++) std::swap(Vt[i * n + k], Vt[j * n + k]);
+        }
+    }
+    for (int i = 0; i < n; i++) Wout[i] = W[i];
+    for (int i = 0; i < n; i++) {
+        const double s = W[i] > minval ? 1 / W[i] : 0.;
+        for (int k = 0; k < m; k++) At[i * m + k] *= s;
+    }
+}
+
+// cvRodrigues2 3x3 -> 3x1 then 3x1 -> 3x3 (projectPoint, utils.py:242-243).
+void rodrigues_roundtrip(const double* Rin, double* Rout) {
+    double At[9], W[3], Vt[9], U[9], R[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) At[i * 3 + j] = Rin[j * 3 + i];
+    jacobi_svd(At, W, Vt, 3, 3);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) U[i * 3 + j] = At[j * 3 + i];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += U[i * 3 + k] * Vt[k * 3 + j];
+            R[i * 3 + j] = s;
+        }
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = std::acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t = (R[0] + 1) * 0.5;
+            rx = std::sqrt(std::max(t, 0.));
+            t = (R[4] + 1) * 0.5;
+            ry = std::sqrt(std::max(t, 0.)) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = std::sqrt(std::max(t, 0.)) * (R[2] < 0 ? -1. : 1.);
+            if (std::fabs(rx) < std::fabs(ry) && std::fabs(rx) < std::fabs(rz) &&
+                (R[5] > 0) != (ry * rz > 0))
+                rz = -rz;
+            theta /= std::sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta;
+            ry *= theta;
+            rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= theta;
+        rx *= vth;
+        ry *= vth;
+        rz *= vth;
+    }
+    // 3x1 -> 3x3
+    const double th = std::sqrt(rx * rx + ry * ry + rz * rz);
+    if (th < DBL_EPSILON) {
+        for (int i = 0; i < 9; i++) Rout[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    // glibc sincos(): the gcc -O2 lowering of OpenCV's adjacent cos/sin calls
+    double ss, cc;
+    ::sincos(th, &ss, &cc);
+    const double c1 = 1. - cc;
+    const double ith = th ? 1. / th : 0.;
+    rx *= ith;
+    ry *= ith;
+    rz *= ith;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double r_x[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    for (int i = 0; i < 9; i++) {
+        const double e = (i % 4 == 0) ? 1.0 : 0.0;
+        Rout[i] = (cc * e + c1 * rrt[i]) + ss * r_x[i];
+    }
+}
+
+// cvTriangulatePoints for one correspondence (utils.py:238-239).
+void triangulate(const double* P1, const double* P2, const double* x1, const double* x2, double* X4) {
+    double A[16];
+    const double* P[2] = {P1, P2};
+    const double* pt[2] = {x1, x2};
+    for (int j = 0; j < 2; j++) {
+        const double x = pt[j][0], y = pt[j][1];
+        for (int k = 0; k < 4; k++) {
+            A[(j * 2 + 0) * 4 + k] = x * P[j][8 + k] - P[j][0 + k];
+            A[(j * 2 + 1) * 4 + k] = y * P[j][8 + k] - P[j][4 + k];
+        }
+    }
+    double At[16], W[4], Vt[16];
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) At[i * 4 + j] = A[j * 4 + i];
+    jacobi_svd(At, W, Vt, 4, 4);
+    for (int k = 0; k < 4; k++) X4[k] = Vt[12 + k];
+}
+
+inline double fma_dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
+    // numpy 3-element dot / matvec row as OpenBLAS 0.3.29 evaluates it
+    return std::fma(a2, b2, std::fma(a1, b1, a0 * b0));
+}
+
+inline int py_wrap(long i, long n) { return (int)(i < 0 ? i + n : i); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Context
+// ---------------------------------------------------------------------------
+
+struct mvs_ctx {
+    int device = 0;
+    int V = 0, H = 0, W = 0, Wq = 0;
+    hipStream_t stream = nullptr;
+    std::vector<CamDev> cams;
+    std::vector<double> K;   // V*9 as given (getProjectionMatrix uses all of K)
+    std::vector<uint8_t> h_rgb;
+    DevBuf<uint8_t> d_rgb, d_stack;
+    DevBuf<CamDev> d_cams;
+    DevBuf<int32_t> d_exact;
+    SceneDev sc{};
+    // scratch for host-pointer scoring
+    DevBuf<double> s_c, s_xy, s_avg;
+    DevBuf<int32_t> s_ref, s_count;
+    DevBuf<uint64_t> s_mask;
+    std::string err;
+    int words() const { return (V + 63) / 64; }
+};
+
+struct mvs_stage_result {
+    std::vector<double> initial, all;
+    int64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
+namespace {
+
+void build_cameras(mvs_ctx* ctx, const double* K, const double* R, const double* t, const double* Rp) {
+    ctx->cams.resize(ctx->V);
+    for (int v = 0; v < ctx->V; ++v) {
+        CamDev& c = ctx->cams[v];
+        std::memset(&c, 0, sizeof c);
+        const double* Kv = K + 9 * v;
+        const double* Rv = R + 9 * v;
+        const double* tv = t + 3 * v;
+        if (Rp)
+            std::memcpy(c.Rp, Rp + 9 * v, sizeof c.Rp);
+        else
+            rodrigues_roundtrip(Rv, c.Rp);
+        std::memcpy(c.t, tv, sizeof c.t);
+        std::memcpy(c.R, Rv, sizeof c.R);
+        c.fx = Kv[0];
+        c.fy = Kv[4];
+        c.cx = Kv[2];
+        c.cy = Kv[5];
+        c.fbar = (Kv[0] + Kv[4]) / 2;
+        for (int j = 0; j < 3; ++j) {
+            // camera_pos = -(R^T @ t) (MVS2.py:189); C = (-R^T) @ t (MVS2.py:351)
+            c.O[j] = -fma_dot3(Rv[j], Rv[3 + j], Rv[6 + j], tv[0], tv[1], tv[2]);
+            c.C[j] = fma_dot3(-Rv[j], -Rv[3 + j], -Rv[6 + j], tv[0], tv[1], tv[2]);
+        }
+    }
+}
+
+int set_err(mvs_ctx* ctx, const Fail& f) {
+    if (ctx) ctx->err = f.msg;
+    g_err = f.msg;
+    return f.code;
+}
+
+template <class Fn>
+int guarded(mvs_ctx* ctx, Fn&& fn) {
+    try {
+        if (ctx) HIPCHK(hipSetDevice(ctx->device));
+        return fn();
+    } catch (const Fail& f) {
+        return set_err(ctx, f);
+    } catch (const std::bad_alloc&) {
+        return set_err(ctx, Fail{MVS_E_NOMEM, "host allocation failed"});
+    } catch (const std::exception& e) {
+        return set_err(ctx, Fail{MVS_E_ARG, e.what()});
+    }
+}
+
+void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
+                  double thr, double* d_xy, uint64_t* d_mask, int32_t* d_count, double* d_avg,
+                  hipStream_t s) {
+    if (wid < 1 || wid > MVS_MAX_WID) throw Fail{MVS_E_UNSUPPORTED, "wid must be in 1..5"};
+    ScoreArgs a{};
+    a.n = n;
+    a.c = d_c;
+    a.ref = d_ref;
+    a.thr = thr;
+    a.xy = d_xy;
+    a.mask = d_mask;
+    a.count = d_count;
+    a.avg = d_avg;
+    a.exact_hits = ctx->d_exact.p;
+    if (mvs_launch_score(&ctx->sc, &a, wid, s) != 0) throw Fail{MVS_E_HIP, "score launch failed"};
+}
+
+// ---------------------------------------------------------------------------
+// Stage engine: seeding + ordered expansion commit
+// ---------------------------------------------------------------------------
+
+struct Engine {
+    mvs_ctx* ctx;
+    int V, words, cs, wid, vlb;
+    double scale;
+    int nci, ncj;
+    int64_t max_pops;
+    hipStream_t s;
+
+    // record table (device) + host mirror
+    DevBuf<double> d_c, d_n, d_xy;
+    DevBuf<uint64_t> d_mask;
+    DevBuf<int32_t> d_R, d_count, d_cell;
+    DevBuf<uint8_t> d_color, d_accept;
+    DevBuf<ChildJob> d_jobs;
+    int64_t nrec = 0, cap = 0;
+    std::vector<uint64_t> h_mask;
+    std::vector<int32_t> h_count, h_cell;
+    std::vector<uint8_t> h_accept, h_enq;
+    std::vector<int64_t> h_child;   // first child record, -1 = unscored
+
+    std::vector<uint8_t> table;     // V*nci*ncj, 1 = vacant (CellTable)
+    std::vector<int32_t> events;    // accepted patch objects, in fill order
+    int64_t n_seeds = 0;
+    int64_t stat_tests = 0, stat_scored = 0, stat_sweeps = 0, stat_seed_cands = 0;
+
+    RecordsDev recs() {
+        RecordsDev r;
+        r.c = d_c.p; r.n = d_n.p; r.xy = d_xy.p; r.mask = d_mask.p; r.R = d_R.p;
+        r.count = d_count.p; r.color = d_color.p; r.accept = d_accept.p; r.cell = d_cell.p;
+        return r;
+    }
+
+    void reserve(int64_t need) {
+        if (need <= cap) return;
+        int64_t nc = std::max<int64_t>(need, std::max<int64_t>(cap * 2, 1 << 16));
+        d_c.grow(nc * 3, nrec * 3, s);
+        d_n.grow(nc * 3, nrec * 3, s);
+        d_xy.grow(nc * 2, nrec * 2, s);
+        d_mask.grow(nc * words, nrec * words, s);
+        d_R.grow(nc, nrec, s);
+        d_count.grow(nc, nrec, s);
+        d_cell.grow(nc * 2, nrec * 2, s);
+        d_color.grow(nc * 4, nrec * 4, s);
+        d_accept.grow(nc, nrec, s);
+        cap = nc;
+        h_mask.resize(nc * words);
+        h_count.resize(nc);
+        h_cell.resize(nc * 2);
+        h_accept.resize(nc);
+        h_enq.resize(nc);
+        h_child.resize(nc, -1);
+    }
+
+    bool vacant(int v, long ci, long cj) const {
+        if (ci >= nci || ci < 0) return false;
+        if (cj >= ncj || cj < 0) return false;
+        return table[((int64_t)v * nci + ci) * ncj + cj] != 0;
+    }
+
+    // CellTable.fill_with_point for every V entry of record r (MVS2.py:98-107,
+    // 258-259, 401-402); the Q-table side is reconstructed from `events`.
+    void fill_record(int64_t r) {
+        const int cx = h_cell[2 * r], cy = h_cell[2 * r + 1];
+        for (int w = 0; w < words; ++w) {
+            uint64_t m = h_mask[r * words + w];
+            while (m) {
+                const int v = 64 * w + __builtin_ctzll(m);
+                m &= m - 1;
+                if (cx >= 0 && cx < nci && cy >= 0 && cy < ncj)
+                    table[((int64_t)v * nci + cx) * ncj + cy] = 0;
+            }
+        }
+    }
+
+    void fetch_range(int64_t first, int64_t n) {
+        if (n == 0) return;
+        HIPCHK(hipMemcpyAsync(h_mask.data() + first * words, d_mask.p + first * words,
+                              n * words * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(h_count.data() + first, d_count.p + first, n * sizeof(int32_t),
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(h_cell.data() + 2 * first, d_cell.p + 2 * first,
+                              2 * n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(h_accept.data() + first, d_accept.p + first, n * sizeof(uint8_t),
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+
+    // ---- seeding: MVS2.py:205-260 ----
+    void seed(int64_t n_tracks, const int64_t* off, const int32_t* ov, const float* oxy) {
+        const std::vector<CamDev>& cams = ctx->cams;
+        struct Cand {
+            double key[5];
+            double c[3], n[3];
+            uint8_t color[3];
+            int R;
+        };
+        std::vector<std::vector<Cand>> per_track(n_tracks);
+        const int H = ctx->H, W = ctx->W;
+        for (int64_t tr = 0; tr < n_tracks; ++tr) {
+            const int64_t o0 = off[tr], o1 = off[tr + 1];
+            if (o1 - o0 < 1) continue;
+            const int Rr = ov[o0];
+            if (Rr < 0 || Rr >= V) throw Fail{MVS_E_ARG, "track view index out of range"};
+            const double base[2] = {(double)oxy[2 * o0], (double)oxy[2 * o0 + 1]};
+            const double* O = cams[Rr].O;
+            for (int64_t o = o0 + 1; o < o1; ++o) {
+                const int k = ov[o];
+                if (k < 0 || k >= V) throw Fail{MVS_E_ARG, "track view index out of range"};
+                double P1[12], P2[12];
+                // getProjectionMatrix = K @ [r|t] (utils.py:234-236)
+                for (int rr = 0; rr < 3; ++rr)
+                    for (int cc = 0; cc < 4; ++cc) {
+                        const CamDev& a = cams[Rr];
+                        const CamDev& b = cams[k];
+                        auto e = [&](const CamDev& m, int q) { return cc < 3 ? m.R[3 * q + cc] : m.t[q]; };
+                        P1[rr * 4 + cc] = fma_dot3(kmat(Rr, rr, 0), kmat(Rr, rr, 1), kmat(Rr, rr, 2),
+                                                   e(a, 0), e(a, 1), e(a, 2));
+                        P2[rr * 4 + cc] = fma_dot3(kmat(k, rr, 0), kmat(k, rr, 1), kmat(k, rr, 2),
+                                                   e(b, 0), e(b, 1), e(b, 2));
+                    }
+                const double pt[2] = {(double)oxy[2 * o], (double)oxy[2 * o + 1]};
+                double X4[4];
+                triangulate(P1, P2, base, pt, X4);
+                Cand cd;
+                for (int q = 0; q < 3; ++q) cd.c[q] = X4[3] == 0 ? 0 * X4[q] : X4[q] / X4[3];
+                const double d0 = cd.c[0] - O[0], d1 = cd.c[1] - O[1], d2 = cd.c[2] - O[2];
+                const double dist = std::sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+                for (int q = 0; q < 3; ++q) cd.n[q] = (O[q] - cd.c[q]) / dist;
+                // get_color(imgs[k], x, y) = img[int(y)][int(x)] (MVS2.py:248)
+                const long xi = (long)oxy[2 * o], yi = (long)oxy[2 * o + 1];
+                const int yy = py_wrap(yi, H), xx = py_wrap(xi, W);
+                if (yy < 0 || yy >= H || xx < 0 || xx >= W) throw Fail{MVS_E_ARG, "observation outside image"};
+                const uint8_t* px = ctx->h_rgb.data() + (((int64_t)k * H + yy) * W + xx) * 3;
+                cd.color[0] = px[0]; cd.color[1] = px[1]; cd.color[2] = px[2];
+                cd.R = Rr;
+                cd.key[0] = dist; cd.key[1] = cd.c[0]; cd.key[2] = cd.c[1]; cd.key[3] = cd.c[2];
+                cd.key[4] = Rr;
+                per_track[tr].push_back(cd);
+            }
+            // MyPatchHeapSort pops in increasing (dist, c0, c1, c2, R) (MVS2.py:13-31)
+            std::stable_sort(per_track[tr].begin(), per_track[tr].end(), [](const Cand& a, const Cand& b) {
+                for (int q = 0; q < 5; ++q) {
+                    if (a.key[q] < b.key[q]) return true;
+                    if (a.key[q] > b.key[q]) return false;
+                }
+                return false;
+            });
+        }
+        // score every seed candidate in one batch (thr 0.4, MVS2.py:255)
+        std::vector<double> hc;
+        std::vector<int32_t> hr;
+        for (auto& v : per_track)
+            for (auto& cd : v) {
+                hc.insert(hc.end(), cd.c, cd.c + 3);
+                hr.push_back(cd.R);
+            }
+        const int64_t nc = (int64_t)hr.size();
+        stat_seed_cands = nc;
+        DevBuf<double> dc, dxy, davg;
+        DevBuf<int32_t> dr, dcount;
+        DevBuf<uint64_t> dmask;
+        dc.alloc(nc * 3); dxy.alloc(nc * 2); davg.alloc(nc); dr.alloc(nc); dcount.alloc(nc);
+        dmask.alloc(nc * words);
+        std::vector<double> xy(nc * 2);
+        std::vector<uint64_t> mask(nc * words);
+        std::vector<int32_t> count(nc);
+        if (nc) {
+            HIPCHK(hipMemcpyAsync(dc.p, hc.data(), nc * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(dr.p, hr.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            score_device(ctx, nc, dc.p, dr.p, wid, 0.4, dxy.p, dmask.p, dcount.p, davg.p, s);
+            HIPCHK(hipMemcpyAsync(xy.data(), dxy.p, nc * 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(mask.data(), dmask.p, nc * words * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(count.data(), dcount.p, nc * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        stat_scored += nc;
+        // first candidate (heap order) with |V| >= vlb is the track's patch
+        std::vector<double> rc, rn, rxy;
+        std::vector<uint8_t> rcol;
+        std::vector<int32_t> rR, rcount, rcell;
+        std::vector<uint64_t> rmask;
+        int64_t idx = 0;
+        for (auto& v : per_track) {
+            int64_t first = idx;
+            idx += (int64_t)v.size();
+            for (size_t q = 0; q < v.size(); ++q) {
+                const int64_t i = first + (int64_t)q;
+                stat_tests++;
+                if (count[i] >= vlb) {
+                    const Cand& cd = v[q];
+                    rc.insert(rc.end(), cd.c, cd.c + 3);
+                    rn.insert(rn.end(), cd.n, cd.n + 3);
+                    rxy.insert(rxy.end(), &xy[2 * i], &xy[2 * i] + 2);
+                    rcol.insert(rcol.end(), {cd.color[0], cd.color[1], cd.color[2], 0});
+                    rR.push_back(cd.R);
+                    rcount.push_back(count[i]);
+                    rmask.insert(rmask.end(), &mask[i * words], &mask[i * words] + words);
+                    rcell.push_back((int32_t)std::floor(xy[2 * i] / cs));
+                    rcell.push_back((int32_t)std::floor(xy[2 * i + 1] / cs));
+                    break;
+                }
+            }
+        }
+        n_seeds = (int64_t)rR.size();
+        reserve(std::max<int64_t>(n_seeds, 1));
+        if (n_seeds) {
+            std::vector<uint8_t> acc(n_seeds, 1);
+            HIPCHK(hipMemcpyAsync(d_c.p, rc.data(), n_seeds * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_n.p, rn.data(), n_seeds * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_xy.p, rxy.data(), n_seeds * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_mask.p, rmask.data(), n_seeds * words * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_R.p, rR.data(), n_seeds * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_count.p, rcount.data(), n_seeds * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_cell.p, rcell.data(), n_seeds * 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_color.p, rcol.data(), n_seeds * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d_accept.p, acc.data(), n_seeds, hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+            std::copy(rmask.begin(), rmask.end(), h_mask.begin());
+            std::copy(rcount.begin(), rcount.end(), h_count.begin());
+            std::copy(rcell.begin(), rcell.end(), h_cell.begin());
+            std::fill(h_accept.begin(), h_accept.begin() + n_seeds, 1);
+        }
+        nrec = n_seeds;
+        for (int64_t r = 0; r < n_seeds; ++r) {
+            fill_record(r);
+            events.push_back((int32_t)r);
+        }
+    }
+
+    double kmat(int v, int r, int c) const { return ctx->K[9 * v + 3 * r + c]; }
+
+    // ---- patch_expansion: MVS2.py:308-404 ----
+    void expand() {
+        std::vector<int32_t> queue;
+        queue.reserve(1 << 20);
+        size_t qhead = 0;
+        std::vector<int32_t> unscored;   // records in order of first enqueue
+        size_t ucur = 0;
+        for (int64_t r = 0; r < n_seeds; ++r) {
+            queue.push_back((int32_t)r);
+            unscored.push_back((int32_t)r);
+            h_enq[r] = 1;
+        }
+        int64_t pops = 0;
+        std::vector<ChildJob> jobs;
+        const double dist_thr = 0.05 / scale;
+        while (true) {
+            // ordered commit until the FIFO head has no scored children
+            while (qhead < queue.size() && pops < max_pops) {
+                const int32_t r = queue[qhead];
+                const int64_t base = h_child[r];
+                if (base < 0) break;
+                ++qhead;
+                ++pops;
+                const long ci = h_cell[2 * r], cj = h_cell[2 * r + 1];
+                int h = 0;
+                for (int w = 0; w < words; ++w) {
+                    uint64_t m = h_mask[(int64_t)r * words + w];
+                    while (m) {
+                        const int v = 64 * w + __builtin_ctzll(m);
+                        m &= m - 1;
+                        for (int i = -1; i <= 1; i += 2) {
+                            const int64_t child = base + 2 * h + (i > 0 ? 1 : 0);
+                            for (int j = -1; j <= 1; j += 2) {
+                                if (!vacant(v, ci + i, cj + j)) continue;
+                                ++stat_tests;
+                                if (h_accept[child]) {
+                                    fill_record(child);
+                                    events.push_back((int32_t)child);
+                                    for (int k = 0; k < h_count[child]; ++k) queue.push_back((int32_t)child);
+                                    if (!h_enq[child]) {
+                                        h_enq[child] = 1;
+                                        unscored.push_back((int32_t)child);
+                                    }
+                                    break;
+                                }
+                            }
+                        }
+                        ++h;
+                    }
+                }
+            }
+            if (qhead >= queue.size() || pops >= max_pops) break;
+            // sweep: score the children of the next unscored records
+            const int64_t remaining = max_pops - pops;
+            int64_t want = std::min<int64_t>(std::max<int64_t>(remaining / 4, 2048), 262144);
+            want = std::min<int64_t>(want, (int64_t)(unscored.size() - ucur));
+            jobs.clear();
+            const int64_t first = nrec;
+            for (int64_t k = 0; k < want; ++k) {
+                const int32_t r = unscored[ucur + k];
+                h_child[r] = first + (int64_t)jobs.size();
+                for (int w = 0; w < words; ++w) {
+                    uint64_t m = h_mask[(int64_t)r * words + w];
+                    while (m) {
+                        const int v = 64 * w + __builtin_ctzll(m);
+                        m &= m - 1;
+                        jobs.push_back(ChildJob{r, (int16_t)v, (int16_t)-1});
+                        jobs.push_back(ChildJob{r, (int16_t)v, (int16_t)1});
+                    }
+                }
+            }
+            ucur += want;
+            const int64_t nj = (int64_t)jobs.size();
+            reserve(nrec + nj);
+            d_jobs.ensure(nj);
+            if (nj) {
+                HIPCHK(hipMemcpyAsync(d_jobs.p, jobs.data(), nj * sizeof(ChildJob), hipMemcpyHostToDevice, s));
+                ExpandArgs a{};
+                a.n = nj;
+                a.first_out = first;
+                a.jobs = d_jobs.p;
+                a.cell_size = cs;
+                a.vlb = vlb;
+                a.dist_thr = dist_thr;
+                a.thr = 0.7;
+                a.exact_hits = ctx->d_exact.p;
+                if (mvs_launch_expand(&ctx->sc, recs(), &a, wid, s) != 0)
+                    throw Fail{MVS_E_HIP, "expand launch failed"};
+                nrec += nj;
+                fetch_range(first, nj);
+            }
+            stat_scored += nj;
+            stat_sweeps++;
+        }
+        stat_pops = pops;
+        stat_queue_left = (int64_t)(queue.size() - qhead);
+    }
+    int64_t stat_pops = 0, stat_queue_left = 0;
+
+    // reconstruct_from_Q order (MVS2.py:159-173): key (view, ci, cj)
+    // lexicographic, append order within a key, first sight of each object.  A
+    // patch is appended under (u, cell) for every u in its V list, so its first
+    // sight is at (min u, cell), in fill order among equal keys.
+    void output(mvs_stage_result* res) {
+        std::vector<double> hc(nrec * 3);
+        std::vector<uint8_t> hcol(nrec * 4);
+        if (nrec) {
+            HIPCHK(hipMemcpyAsync(hc.data(), d_c.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(hcol.data(), d_color.p, nrec * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        auto row = [&](std::vector<double>& out, int64_t r) {
+            out.push_back(hc[3 * r]); out.push_back(hc[3 * r + 1]); out.push_back(hc[3 * r + 2]);
+            out.push_back(hcol[4 * r]); out.push_back(hcol[4 * r + 1]); out.push_back(hcol[4 * r + 2]);
+        };
+        for (int64_t r = 0; r < n_seeds; ++r) row(res->initial, r);
+        std::vector<std::pair<int64_t, int64_t>> keyed;   // (key, event index)
+        keyed.reserve(events.size());
+        for (size_t e = 0; e < events.size(); ++e) {
+            const int64_t r = events[e];
+            int minv = -1;
+            for (int w = 0; w < words && minv < 0; ++w)
+                if (h_mask[r * words + w]) minv = 64 * w + __builtin_ctzll(h_mask[r * words + w]);
+            const int cx = h_cell[2 * r], cy = h_cell[2 * r + 1];
+            if (minv < 0 || cx < 0 || cx >= nci || cy < 0 || cy >= ncj) continue;
+            keyed.emplace_back(((int64_t)minv * nci + cx) * ncj + cy, (int64_t)e);
+        }
+        std::sort(keyed.begin(), keyed.end());
+        res->all.reserve(keyed.size() * 6);
+        for (auto& k : keyed) row(res->all, events[k.second]);
+        res->stats[0] = stat_pops;
+        res->stats[1] = stat_tests;
+        res->stats[2] = (int64_t)events.size();
+        res->stats[3] = stat_queue_left;
+        res->stats[4] = stat_scored;
+        res->stats[5] = stat_sweeps;
+        res->stats[6] = stat_seed_cands;
+    }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+
+extern "C" {
+
+const char* mvs_version(void) { return "mvs_amd 0.1 (gfx950)"; }
+
+const char* mvs_last_error(const mvs_ctx* ctx) {
+    return ctx ? ctx->err.c_str() : g_err.c_str();
+}
+
+int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const double* K,
+                   const double* R, const double* t, const double* Rp, mvs_ctx** out) {
+    if (!out || !rgb || !K || !R || !t) return set_err(nullptr, Fail{MVS_E_ARG, "null argument"});
+    *out = nullptr;
+    if (V < 1 || V > MVS_MAX_VIEWS || H < 16 || W < 16)
+        return set_err(nullptr, Fail{MVS_E_UNSUPPORTED, "need 1 <= V <= 256 and H, W >= 16"});
+    std::unique_ptr<mvs_ctx> ctx(new mvs_ctx());
+    ctx->device = device;
+    int rc = guarded(ctx.get(), [&]() {
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev) throw Fail{MVS_E_ARG, "no such HIP device"};
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->V = V; ctx->H = H; ctx->W = W;
+        ctx->Wq = (W + 3) / 4 + 1;   // +1 zero quad: the last aligned dword read of a row
+        const int64_t npx = (int64_t)V * H * W;
+        ctx->h_rgb.assign(rgb, rgb + npx * 3);
+        ctx->d_rgb.alloc(npx * 3);
+        HIPCHK(hipMemcpyAsync(ctx->d_rgb.p, rgb, npx * 3, hipMemcpyHostToDevice, ctx->stream));
+        const int64_t stack_bytes = (int64_t)H * ctx->Wq * V * 4;
+        ctx->d_stack.alloc(stack_bytes + 64);
+        HIPCHK(hipMemsetAsync(ctx->d_stack.p, 0, stack_bytes + 64, ctx->stream));
+        if (mvs_launch_build_stack(ctx->d_rgb.p, ctx->d_stack.p, V, H, W, ctx->Wq, ctx->stream) != 0)
+            throw Fail{MVS_E_HIP, "build_stack launch failed"};
+        build_cameras(ctx.get(), K, R, t, Rp);
+        ctx->K.assign(K, K + 9 * V);
+        ctx->d_cams.alloc(V);
+        HIPCHK(hipMemcpyAsync(ctx->d_cams.p, ctx->cams.data(), V * sizeof(CamDev), hipMemcpyHostToDevice, ctx->stream));
+        ctx->d_exact.alloc(1);
+        HIPCHK(hipMemsetAsync(ctx->d_exact.p, 0, sizeof(int32_t), ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        ctx->sc.V = V; ctx->sc.H = H; ctx->sc.W = W; ctx->sc.Wq = ctx->Wq;
+        ctx->sc.row_bytes = (int64_t)ctx->Wq * V * 4;
+        ctx->sc.stack = ctx->d_stack.p;
+        ctx->sc.rgb = ctx->d_rgb.p;
+        ctx->sc.cams = ctx->d_cams.p;
+        return 0;
+    });
+    if (rc != 0) {
+        g_err = ctx->err;
+        return rc;
+    }
+    *out = ctx.release();
+    return 0;
+}
+
+void mvs_ctx_destroy(mvs_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp) {
+    if (!ctx || !Rp) return MVS_E_ARG;
+    for (int v = 0; v < ctx->V; ++v) std::memcpy(Rp + 9 * v, ctx->cams[v].Rp, 9 * sizeof(double));
+    return 0;
+}
+
+int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
+                     double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
+                     double* d_avg, void* stream) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (n < 0) return set_err(ctx, Fail{MVS_E_ARG, "n < 0"});
+    return guarded(ctx, [&]() {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        score_device(ctx, n, d_c, d_ref, wid, min_ncc, d_xy, d_mask, d_count, d_avg, s);
+        return 0;
+    });
+}
+
+int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int wid, double min_ncc,
+              double* xy, uint64_t* mask, int32_t* count, double* avg) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (n < 0 || (n > 0 && (!c || !ref || !xy || !mask || !count || !avg)))
+        return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
+    return guarded(ctx, [&]() {
+        for (int64_t i = 0; i < n; ++i)
+            if (ref[i] < 0 || ref[i] >= ctx->V) throw Fail{MVS_E_ARG, "ref view out of range"};
+        if (n == 0) return 0;
+        hipStream_t s = ctx->stream;
+        const int words = ctx->words();
+        ctx->s_c.ensure(n * 3); ctx->s_ref.ensure(n); ctx->s_xy.ensure(n * 2);
+        ctx->s_mask.ensure(n * words); ctx->s_count.ensure(n); ctx->s_avg.ensure(n);
+        HIPCHK(hipMemcpyAsync(ctx->s_c.p, c, n * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(ctx->s_ref.p, ref, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        score_device(ctx, n, ctx->s_c.p, ctx->s_ref.p, wid, min_ncc, ctx->s_xy.p, ctx->s_mask.p,
+                     ctx->s_count.p, ctx->s_avg.p, s);
+        HIPCHK(hipMemcpyAsync(xy, ctx->s_xy.p, n * 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(mask, ctx->s_mask.p, n * words * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(count, ctx->s_count.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(avg, ctx->s_avg.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    });
+}
+
+int64_t mvs_exact_hits(mvs_ctx* ctx) {
+    if (!ctx) return MVS_E_ARG;
+    int32_t h = 0;
+    int rc = guarded(ctx, [&]() {
+        HIPCHK(hipMemcpyAsync(&h, ctx->d_exact.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        return 0;
+    });
+    return rc ? rc : h;
+}
+
+int mvs_ncc_windows(int64_t n, int npx, const uint8_t* d_a, const uint8_t* d_b, double thr,
+                    int force_exact, double* d_ncc, uint8_t* d_pass, void* stream) {
+    if (npx < 1 || npx > 128) return set_err(nullptr, Fail{MVS_E_UNSUPPORTED, "npx must be in 1..128"});
+    int rc = mvs_launch_ncc_windows(n, npx, d_a, d_b, thr, force_exact, d_ncc, d_pass, (hipStream_t)stream);
+    if (rc) return set_err(nullptr, Fail{MVS_E_HIP, "ncc_windows launch failed"});
+    return 0;
+}
+
+int mvs_stage_run(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off, const int32_t* obs_view,
+                  const float* obs_xy, int cell_size, double scale, int wid, int64_t max_pops,
+                  mvs_stage_result** out) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (!out || n_tracks < 0 || (n_tracks > 0 && (!track_off || !obs_view || !obs_xy)) || cell_size < 1)
+        return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
+    if (wid != 3 && wid != 5) return set_err(ctx, Fail{MVS_E_UNSUPPORTED, "stage supports wid 3 or 5"});
+    *out = nullptr;
+    return guarded(ctx, [&]() {
+        std::unique_ptr<mvs_stage_result> res(new mvs_stage_result());
+        std::unique_ptr<Engine> E(new Engine());
+        E->ctx = ctx;
+        E->V = ctx->V;
+        E->words = ctx->words();
+        E->cs = cell_size;
+        E->wid = wid;
+        E->vlb = ctx->V > 2 ? 3 : 2;   // MVS2.py:200-203
+        E->scale = scale;
+        // CellTable: ceil((W-1)/cs) x ceil((H-1)/cs) per view (MVS2.py:88)
+        E->nci = (int)std::ceil((double)(ctx->W - 1) / cell_size);
+        E->ncj = (int)std::ceil((double)(ctx->H - 1) / cell_size);
+        E->max_pops = std::min<int64_t>(std::max<int64_t>(max_pops, 0), 100000);   // MVS2.py:321
+        E->s = ctx->stream;
+        E->table.assign((size_t)ctx->V * E->nci * E->ncj, 1);
+        HIPCHK(hipMemsetAsync(ctx->d_exact.p, 0, sizeof(int32_t), ctx->stream));
+        E->seed(n_tracks, track_off, obs_view, obs_xy);
+        E->expand();
+        E->output(res.get());
+        int32_t h = 0;
+        HIPCHK(hipMemcpyAsync(&h, ctx->d_exact.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        res->stats[7] = h;
+        *out = res.release();
+        return 0;
+    });
+}
+
+int64_t mvs_stage_count(const mvs_stage_result* res, int which) {
+    if (!res) return MVS_E_ARG;
+    return (int64_t)((which ? res->all.size() : res->initial.size()) / 6);
+}
+
+int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows) {
+    if (!res || !rows) return MVS_E_ARG;
+    const std::vector<double>& v = which ? res->all : res->initial;
+    std::memcpy(rows, v.data(), v.size() * sizeof(double));
+    return 0;
+}
+
+int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats) {
+    if (!res || !stats) return MVS_E_ARG;
+    std::memcpy(stats, res->stats, sizeof res->stats);
+    return 0;
+}
+
+void mvs_stage_free(mvs_stage_result* res) { delete res; }
+
+int mvs_rodrigues_roundtrip(const double* R, double* Rp) {
+    if (!R || !Rp) return MVS_E_ARG;
+    rodrigues_roundtrip(R, Rp);
+    return 0;
+}
+
+int mvs_triangulate(const double* P1, const double* P2, const double* x1, const double* x2, double* X4) {
+    if (!P1 || !P2 || !x1 || !x2 || !X4) return MVS_E_ARG;
+    triangulate(P1, P2, x1, x2, X4);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// Internal declarations shared by the HIP kernels (mvs_kernels.hip) and the
+// host engine (mvs_engine.cpp).  Not part of the public C-ABI (include/mvs_amd.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MVS_MAX_VIEWS 256
+#define MVS_MAX_WID 5
+
+// Per-view camera constants, laid out for wave-uniform (scalar) loads.
+// All values are computed on the host in the reference's operation order
+// (see mvs_engine.cpp: build_cameras).
+struct CamDev {
+    double Rp[9];   // Rodrigues round-trip of R (what cv2.projectPoints uses, utils.py:242-243)
+    double t[3];
+    double fx, fy, cx, cy;   // OpenCV projectPoints reads a[0], a[4], a[2], a[5]
+    double R[9];    // par-file rotation (MVS2.py:351-353)
+    double O[3];    // camera_pos = -(R^T t)      (MVS2.py:189)
+    double C[3];    // (-R^T) @ t                 (MVS2.py:351)
+    double fbar;    // (f_x + f_y)/2              (MVS2.py:353)
+    double pad[3];
+};
+
+// Device-resident scene: the gray stack in quad-interleaved pixel-major
+// layout  stack[y][k][v][4] = gray_v(y, 4k..4k+3)  (k = quad index), so that
+// one window row of every view is one contiguous run, and one dword holds
+// four horizontally adjacent pixels of one view (v_dot4_u32_u8 operand).
+struct SceneDev {
+    int V, H, W;
+    int Wq;            // quads per row, incl. one zero pad quad
+    int64_t row_bytes; // Wq * V * 4
+    const uint8_t* stack;
+    const uint8_t* rgb;      // V*H*W*3 (colour lookups of expansion candidates)
+    const CamDev* cams;
+};
+
+// Inputs/outputs of one scoring batch (device pointers).
+struct ScoreArgs {
+    int64_t n;
+    const double* c;      // n*3
+    const int32_t* ref;   // n
+    double thr;
+    double* xy;           // n*2 (projection into ref view, MVS2.py:63)
+    uint64_t* mask;       // n*words
+    int32_t* count;       // n
+    double* avg;          // n
+    int32_t* exact_hits;  // 1 counter: lanes that took the exact (numpy-order) path
+};
+
+// One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).
+struct ChildJob {
+    int32_t parent;
+    int16_t view;
+    int16_t di;
+};
+
+// Record table (device): one row per scored candidate that may become a patch.
+struct RecordsDev {
+    double* c;         // 3
+    double* n;         // 3
+    double* xy;        // 2
+    uint64_t* mask;    // words
+    int32_t* R;
+    int32_t* count;
+    uint8_t* color;    // 4 (rgb + pad)
+    uint8_t* accept;
+    int32_t* cell;     // 2: floor(x/cs), floor(y/cs)
+};
+
+struct ExpandArgs {
+    int64_t n;                 // children in this launch
+    int64_t first_out;         // record index of child 0
+    const ChildJob* jobs;
+    int cell_size;
+    int vlb;
+    double dist_thr;           // 0.05 / scale (MVS2.py:369)
+    double thr;                // 0.7 (MVS2.py:362)
+    int32_t* exact_hits;
+};
+
+extern "C" {
+int mvs_launch_build_stack(const uint8_t* d_rgb, uint8_t* d_stack, int V, int H, int W, int Wq,
+                           hipStream_t s);
+int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s);
+int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, int wid,
+                      hipStream_t s);
+int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
+                           int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
+}

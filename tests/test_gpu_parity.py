@@ -1,0 +1,218 @@
+"""HIP path (libmvs_amd.so on an MI355X) against the oracle and the reference's
+golden vectors.  Bar: bit-exact for projections, masks, counts, accepted
+patch positions/colours/order; avg_ncc_score within 1e-12 (closed-form NCC,
+not numpy's summation order -- avg_ncc_score feeds only the disabled
+filter_out_outlier, MVS2.py:281)."""
+import numpy as np
+import pytest
+
+from conftest import bench_candidates, stage_golden
+
+pytestmark = pytest.mark.gpu
+
+AVG_TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg, dino):
+    import torch
+    assert torch.cuda.is_available(), "GPU test without a GPU"
+    rgb, K, R, t = dino
+    c = pkg.MvsContext(rgb, K, R, t, device=0)
+    yield c
+    c.close()
+
+
+def test_rproj_matches_oracle(ctx, oracle_scene):
+    assert np.array_equal(ctx.rproj().reshape(-1, 9), oracle_scene.Rp)
+
+
+def test_photo_test_vs_reference_golden(ctx, func_golden):
+    f = func_golden
+    for thr in (0.7, 0.4):
+        sel = f["pt_thr"] == thr
+        xy, mask, count, avg = ctx.score(f["pt_c"][sel], f["pt_R"][sel], thr, 5)
+        assert np.array_equal(xy, f["pt_xy"][sel])
+        assert np.array_equal(mask, f["pt_mask"][sel])
+        assert np.array_equal(count, f["pt_count"][sel])
+        np.testing.assert_allclose(avg, f["pt_avg"][sel], rtol=0, atol=AVG_TOL)
+
+
+@pytest.mark.parametrize("wid,thr", [(5, 0.7), (5, 0.4), (3, 0.7), (1, 0.5)])
+def test_score_vs_oracle_bench_batch(ctx, oracle_scene, dino, wid, thr):
+    rgb, K, R, t = dino
+    c, ref = bench_candidates(6000, K, R, t, seed=wid)
+    xy, mask, count, avg = ctx.score(c, ref, thr, wid)
+    oxy, omask, ocount, oavg = oracle_scene.score_batch(c, ref, thr, wid, nthreads=8)
+    assert np.array_equal(xy, oxy)
+    assert np.array_equal(mask, omask)
+    assert np.array_equal(count, ocount)
+    np.testing.assert_allclose(avg, oavg, rtol=0, atol=AVG_TOL)
+    assert count.sum() > 0
+
+
+def test_score_edge_candidates(ctx, oracle_scene, dino):
+    """Windows touching every bound of HarrisFeatures.py:128, points behind the
+    camera, at the camera centre (z = 0 -> OpenCV's 1/z guard) and far away."""
+    rgb, K, R, t = dino
+    rng = np.random.default_rng(7)
+    cs, refs = [], []
+    Kinv = np.linalg.inv(K)
+    for v in range(48):
+        for (x, y) in [(5.9, 100.0), (6.0, 100.0), (6.5, 5.0), (633.9, 472.9), (634.0, 473.0),
+                       (632.99, 4.99), (320.0, 473.99), (-3.0, 200.0), (700.0, 200.0)]:
+            z = rng.uniform(0.6, 0.7)
+            ray = Kinv[v] @ np.array([x, y, 1.0])
+            cs.append(R[v].T @ (z * ray - t[v].ravel())); refs.append(v)
+        O = -(R[v].T @ t[v].ravel())
+        cs.append(O.copy()); refs.append(v)                                       # camera centre
+        cs.append(O - 0.5 * (R[v].T @ np.array([0, 0, 1.0]))); refs.append(v)      # behind
+        cs.append(O + 1e6 * (R[v].T @ np.array([0.1, 0.1, 1.0]))); refs.append(v)  # far
+    c, ref = np.array(cs), np.array(refs, np.int32)
+    got = ctx.score(c, ref, 0.7, 5)
+    exp = oracle_scene.score_batch(c, ref, 0.7, 5)
+    for g, e in zip(got[:3], exp[:3]):
+        assert np.array_equal(g, e)
+
+
+def test_score_empty_batch(ctx):
+    xy, mask, count, avg = ctx.score(np.zeros((0, 3)), np.zeros(0, np.int32))
+    assert len(count) == 0
+
+
+def test_bad_ref_raises(ctx):
+    with pytest.raises(RuntimeError):
+        ctx.score(np.zeros((1, 3)), np.array([48], np.int32))
+
+
+def test_score_device_tensors(ctx, dino, oracle_scene):
+    import torch
+    rgb, K, R, t = dino
+    c, ref = bench_candidates(4096, K, R, t, seed=11)
+    dev = torch.device("cuda:0")
+    tc = torch.from_numpy(c).to(dev)
+    tr = torch.from_numpy(ref).to(dev)
+    xy = torch.empty((len(ref), 2), dtype=torch.float64, device=dev)
+    mask = torch.empty((len(ref), 1), dtype=torch.int64, device=dev)
+    count = torch.empty(len(ref), dtype=torch.int32, device=dev)
+    avg = torch.empty(len(ref), dtype=torch.float64, device=dev)
+    ctx.score_device(tc, tr, xy, mask, count, avg, 0.7, 5,
+                     stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    oxy, omask, ocount, _ = oracle_scene.score_batch(c, ref, 0.7, 5)
+    assert np.array_equal(xy.cpu().numpy(), oxy)
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), omask)
+    assert np.array_equal(count.cpu().numpy(), ocount)
+
+
+@pytest.mark.parametrize("wid", [5, 3])
+def test_ncc_windows_golden(pkg, func_golden, wid):
+    import torch
+    A = torch.from_numpy(func_golden[f"ncc_a_w{wid}"]).cuda()
+    B = torch.from_numpy(func_golden[f"ncc_b_w{wid}"]).cuda()
+    S = func_golden[f"ncc_s_w{wid}"]
+    for thr in (0.7, 0.4, 0.0, -0.5):
+        ncc, ok = pkg.ncc_windows(A, B, thr)
+        exp = np.nan_to_num(S, nan=-np.inf) > thr
+        assert np.array_equal(ok.cpu().numpy().astype(bool), exp)
+        got = ncc.cpu().numpy()
+        fin = ~np.isnan(S)
+        assert np.array_equal(np.isnan(got), ~fin)
+        np.testing.assert_allclose(got[fin], S[fin], rtol=0, atol=1e-13)
+    ncc, ok = pkg.ncc_windows(A, B, 0.7, force_exact=True)   # numpy-order path: bit-exact
+    got = ncc.cpu().numpy()
+    assert np.array_equal(got, S, equal_nan=True)
+
+
+def test_ncc_guard_band_decisions(pkg, orc):
+    """Thresholds placed exactly on the reference's ncc value force the guard
+    path; the decision must be the reference's strict `ncc > thr`."""
+    import torch
+    rng = np.random.default_rng(3)
+    A = rng.integers(0, 256, (2000, 121), dtype=np.uint8)
+    B = np.clip(A.astype(int) + rng.integers(-40, 41, A.shape), 0, 255).astype(np.uint8)
+    ref = np.array([orc.ctncc(a, b) for a, b in zip(A, B)])
+    ta, tb = torch.from_numpy(A).cuda(), torch.from_numpy(B).cuda()
+    for delta in (0.0, 1e-16, -1e-16, 5e-13, -5e-13):
+        for i in range(0, 2000, 200):
+            thr = float(ref[i] + delta)
+            ncc, ok = pkg.ncc_windows(ta[i:i + 1], tb[i:i + 1], thr)
+            assert bool(ok.item()) == bool(ref[i] > thr), (i, delta)
+
+
+@pytest.mark.parametrize("cap", [200, 2000])
+def test_stage_vs_reference_golden(ctx, seeds, cap):
+    g = stage_golden(cap)
+    ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
+                              cell_size=2, scale=10.0, wid=5, max_pops=cap)
+    assert st["pops"] == cap
+    assert np.array_equal(ini, g["initial_patches"])
+    assert allp.shape == g["all_patches"].shape
+    assert np.array_equal(allp, g["all_patches"])
+
+
+@pytest.mark.parametrize("cap", [1, 5000])
+def test_stage_vs_oracle(ctx, oracle_scene, seeds, cap):
+    ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
+                              cell_size=2, scale=10.0, wid=5, max_pops=cap)
+    oini, oall, ost = oracle_scene.mvs_stage(seeds["track_off"], seeds["obs_view"],
+                                             seeds["obs_xy"], max_pops=cap)
+    assert st["pops"] == ost["pops"]
+    assert st["tests"] == ost["tests"]
+    assert st["queue_left"] == ost["queue_left"]
+    assert np.array_equal(ini, oini)
+    assert np.array_equal(allp, oall)
+
+
+def test_stage_cell_size_and_scale_variants(ctx, oracle_scene, seeds):
+    for cs, scale in [(3, 10.0), (2, 1.0)]:
+        ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
+                                  cell_size=cs, scale=scale, wid=5, max_pops=500)
+        oini, oall, ost = oracle_scene.mvs_stage(seeds["track_off"], seeds["obs_view"],
+                                                 seeds["obs_xy"], cell_size=cs, scale=scale,
+                                                 max_pops=500)
+        assert np.array_equal(ini, oini)
+        assert np.array_equal(allp, oall)
+
+
+def test_stage_empty_and_ragged_tracks(ctx, oracle_scene, seeds):
+    # no tracks at all
+    ini, allp, st = ctx.stage(np.array([0], np.int64), np.zeros(0, np.int32),
+                              np.zeros((0, 2), np.float32), max_pops=100)
+    assert len(ini) == 0 and len(allp) == 0
+    # ragged: single-observation tracks (no candidate), 3-view tracks
+    off, view, xy = [0], [], []
+    for k in range(len(seeds["track_off"]) - 1):
+        o0, o1 = seeds["track_off"][k], seeds["track_off"][k + 1]
+        obs = list(range(o0, o1))
+        if k % 5 == 0:
+            obs = obs[:1]
+        elif k % 5 == 1 and k + 1 < len(seeds["track_off"]) - 1:
+            obs = obs + [seeds["track_off"][k + 1] + 1]
+        for o in obs:
+            view.append(seeds["obs_view"][o]); xy.append(seeds["obs_xy"][o])
+        off.append(len(view))
+    args = (np.array(off, np.int64), np.array(view, np.int32), np.array(xy, np.float32))
+    ini, allp, st = ctx.stage(*args, max_pops=300)
+    oini, oall, ost = oracle_scene.mvs_stage(*args, max_pops=300)
+    assert np.array_equal(ini, oini)
+    assert np.array_equal(allp, oall)
+
+
+@pytest.mark.parametrize("V", [5, 100, 256])
+def test_view_count_variants(pkg, orc, V):
+    """Lane-slot layouts: V < 64, one extra slot, and the 4-slot 256-view case."""
+    syn = pkg.synthetic
+    H, W = 96, 128
+    rgb, K, R, t = syn.ring_scene(V=V, H=H, W=W, seed=V)
+    # smooth the textures so that some views pass
+    rgb = ((rgb.astype(np.uint16) + np.roll(rgb, 1, axis=0)) // 2).astype(np.uint8)
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        sc = orc.Scene(rgb, K, R, t)
+        c, ref = syn.candidates(3000, K, R, t, W=W, H=H, seed=1)
+        for thr in (0.2, -0.2):
+            got = cx.score(c, ref, thr, 5)
+            exp = sc.score_batch(c, ref, thr, 5)
+            for g, e in zip(got[:3], exp[:3]):
+                assert np.array_equal(g, e)
+            np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
