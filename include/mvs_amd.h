@@ -101,6 +101,20 @@ int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows);
 int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats);
 void mvs_stage_free(mvs_stage_result* res);
 
+/* patch_expansion candidates (MVS2.py:329-369) for explicit jobs: job k =
+ * (parent job_parent[k], hit view job_view[k], i = job_di[k] in {-1,+1}).
+ * Parents: centre pc, normal pn, pxy = projection into the parent's
+ * reference view (the x, y of its V entries).  Per job: X, nX (n of the new
+ * patch), colour (img[int(cc1)][int(cc0)]), projection xy, mask/count of the
+ * photo test at min_ncc, accept = |V| >= vlb && is_patch_neighbor(0.1) &&
+ * |pc - X| < 0.05/scale.  Host pointers; wid 3 or 5. */
+int mvs_expand_candidates(mvs_ctx* ctx, int64_t n_parents, const double* pc, const double* pn,
+                          const double* pxy, int64_t n_jobs, const int32_t* job_parent,
+                          const int32_t* job_view, const int32_t* job_di, int cell_size,
+                          double scale, int wid, double min_ncc, double* X, double* nX,
+                          uint8_t* color, double* xy, uint64_t* mask, int32_t* count,
+                          uint8_t* accept);
+
 /* Host geometry the stage uses, exported for parity tests:
  * cv2.Rodrigues round trip (utils.py:242-243) and cv2.triangulatePoints for one
  * point (utils.py:238-239, homogeneous 4-vector). */

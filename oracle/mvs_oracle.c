@@ -32,6 +32,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <float.h>
+#include <stdio.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -455,6 +456,50 @@ static int64_t run_photo(const or_scene *S, or_state *st, int64_t pid, double th
     return cnt;
 }
 
+/* One expansion candidate (MVS2.py:329-369) for parent (pc, pn) whose V
+ * entries carry pxy, hit view v, i = di: geometry, photo test (thr), accept
+ * test.  Outputs X, nX, colour, projection, mask, count; returns accept. */
+int or_expand_candidate(const or_scene *S, const double *pc, const double *pn, const double *pxy,
+                        int v, int di, int cell_size, double scale, int wid, double thr,
+                        double *X, double *nX, uint8_t *color, double *xy, uint64_t *mask,
+                        int32_t *count) {
+    const double *K = S->K + 9 * v, *R = S->Rraw + 9 * v, *t = S->t + 3 * v;
+    double O[3];
+    for (int j = 0; j < 3; j++) O[j] = -fma(R[6 + j], t[2], fma(R[3 + j], t[1], R[j] * t[0]));
+    long ci = (long)floor(pxy[0] / cell_size), cj = (long)floor(pxy[1] / cell_size);
+    double cc0 = cell_size * ((double)(ci + di) + 0.5);
+    double cc1 = cell_size * ((double)(cj + di) + 0.5);
+    double Cc[3], w[3], Pw[3], d[3];
+    for (int q = 0; q < 3; q++) Cc[q] = fma(-R[6 + q], t[2], fma(-R[3 + q], t[1], (-R[q]) * t[0]));
+    w[0] = cc0 - K[2]; w[1] = cc1 - K[5]; w[2] = (K[0] + K[4]) / 2;
+    for (int q = 0; q < 3; q++) Pw[q] = fma(R[6 + q], w[2], fma(R[3 + q], w[1], R[q] * w[0])) + Cc[q];
+    double nrm = sqrt((Pw[0] * Pw[0] + Pw[1] * Pw[1]) + Pw[2] * Pw[2]);
+    for (int q = 0; q < 3; q++) d[q] = Pw[q] / nrm;
+    double dot_out = dot3(d, pn);
+    double cmo[3] = {pc[0] - O[0], pc[1] - O[1], pc[2] - O[2]};
+    double tt = dot3(cmo, pn) / dot_out;
+    for (int q = 0; q < 3; q++) X[q] = O[q] + tt * d[q];
+    double e0 = X[0] - O[0], e1 = X[1] - O[1], e2 = X[2] - O[2];
+    double dist = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+    for (int q = 0; q < 3; q++) nX[q] = (O[q] - X[q]) / dist;
+    long cy = (long)cc1, cx = (long)cc0;
+    cy = cy < 0 ? cy + S->H : cy; cx = cx < 0 ? cx + S->W : cx;
+    const uint8_t *px = S->rgb + (((int64_t)v * S->H + cy) * S->W + cx) * 3;
+    color[0] = px[0]; color[1] = px[1]; color[2] = px[2];
+    int32_t Vidx[OR_MAXV];
+    double avg;
+    int cnt = or_photo_test(S, X, v, thr, wid, Vidx, xy, &avg);
+    int words = (S->V + 63) / 64;
+    for (int q = 0; q < words; q++) mask[q] = 0;
+    for (int k = 0; k < cnt; k++) mask[Vidx[k] / 64] |= 1ull << (Vidx[k] % 64);
+    *count = cnt;
+    int vlb = S->V > 2 ? 3 : 2;
+    double pm[3] = {pc[0] - X[0], pc[1] - X[1], pc[2] - X[2]};
+    double nb = fabs(dot3(pm, pn) + dot3(pm, nX));
+    double dd = sqrt((pm[0] * pm[0] + pm[1] * pm[1]) + pm[2] * pm[2]);
+    return cnt >= vlb && nb < 0.1 && dd < 0.05 / scale;
+}
+
 typedef struct { double key[5]; int64_t pid; } heap_item;
 static int cmp_heap(const void *a, const void *b) {
     const heap_item *x = (const heap_item *)a, *y = (const heap_item *)b;
@@ -564,6 +609,7 @@ int or_mvs_stage(const or_scene *S, int64_t n_tracks, const int64_t *track_off, 
     for (int64_t k = 0; k < n_initial; k++) queue[qtail++] = initial[k];
     int64_t iteration = 0;
     double dist_thr = 0.05 / scale;
+    const int trace = getenv("MVS_TRACE") != NULL;
     while (qhead < qtail && iteration < max_pops) {
         iteration++;
         int64_t par = queue[qhead++];
@@ -612,6 +658,9 @@ int or_mvs_stage(const or_scene *S, int64_t n_tracks, const int64_t *track_off, 
                     double nb = fabs(dot3(pm, Pp.n) + dot3(pm, P->n));
                     double g0 = Pp.c[0] - P->c[0], g1 = Pp.c[1] - P->c[1], g2 = Pp.c[2] - P->c[2];
                     double dd = sqrt((g0 * g0 + g1 * g1) + g2 * g2);
+                    if (trace) fprintf(stderr, "O pop %lld rec %lld v %d i %d j %d acc %d cnt %d cell %ld %ld\n",
+                        (long long)iteration, (long long)par, v, i, j, (int)(cnt >= vlb && nb < 0.1 && dd < dist_thr), cnt,
+                        (long)floor(P->x / cell_size), (long)floor(P->y / cell_size));
                     if (cnt >= vlb && nb < 0.1 && dd < dist_thr) {
                         st.accepts++;
                         for (int k = 0; k < P->nV; k++) {

@@ -42,6 +42,10 @@ SIGNATURES = [
     ("mvs_stage_rows", ctypes.c_int, [_vp, ctypes.c_int, _dp]),
     ("mvs_stage_stats", ctypes.c_int, [_vp, _i64p]),
     ("mvs_stage_free", None, [_vp]),
+    ("mvs_expand_candidates", ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, ctypes.c_int64,
+                                             _i32p, _i32p, _i32p, ctypes.c_int, ctypes.c_double,
+                                             ctypes.c_int, ctypes.c_double, _dp, _dp, _u8p, _dp,
+                                             _u64p, _i32p, _u8p]),
     ("mvs_rodrigues_roundtrip", ctypes.c_int, [_dp, _dp]),
     ("mvs_triangulate", ctypes.c_int, [_dp, _dp, _dp, _dp, _dp]),
 ]
@@ -189,6 +193,29 @@ class MvsContext:
                                      ptr(xy), ptr(mask), ptr(count), ptr(avg),
                                      stream if stream is not None else None)
         check(rc, self._h, "mvs_score_device")
+
+    def expand_candidates(self, pc, pn, pxy, job_parent, job_view, job_di, cell_size=2,
+                          scale=10.0, wid=5, min_ncc=0.7):
+        """patch_expansion candidates (MVS2.py:329-369) for explicit jobs (see mvs_amd.h)."""
+        pc = _c(pc, np.float64).reshape(-1, 3)
+        pn = _c(pn, np.float64).reshape(-1, 3)
+        pxy = _c(pxy, np.float64).reshape(-1, 2)
+        jp = _c(job_parent, np.int32)
+        jv = _c(job_view, np.int32)
+        jd = _c(job_di, np.int32)
+        n = len(jp)
+        X, nX, xy = np.empty((n, 3)), np.empty((n, 3)), np.empty((n, 2))
+        color = np.empty((n, 3), np.uint8)
+        mask = np.empty((n, self.words), np.uint64)
+        count = np.empty(n, np.int32)
+        acc = np.empty(n, np.uint8)
+        rc = load().mvs_expand_candidates(self._h, len(pc), _p(pc, _dp), _p(pn, _dp), _p(pxy, _dp),
+                                          n, _p(jp, _i32p), _p(jv, _i32p), _p(jd, _i32p),
+                                          int(cell_size), float(scale), int(wid), float(min_ncc),
+                                          _p(X, _dp), _p(nX, _dp), _p(color, _u8p), _p(xy, _dp),
+                                          _p(mask, _u64p), _p(count, _i32p), _p(acc, _u8p))
+        check(rc, self._h, "mvs_expand_candidates")
+        return X, nX, color, xy, mask, count, acc
 
     def stage(self, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5, max_pops=100000):
         """DensePointsWithMVS2 minus IO; returns (initial N0x6, all Nx6, stats dict)."""

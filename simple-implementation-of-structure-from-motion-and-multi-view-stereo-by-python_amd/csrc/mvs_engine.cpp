@@ -18,6 +18,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -590,6 +591,7 @@ struct Engine {
 
     // ---- patch_expansion: MVS2.py:308-404 ----
     void expand() {
+        const bool trace = std::getenv("MVS_TRACE") != nullptr;
         std::vector<int32_t> queue;
         queue.reserve(1 << 20);
         size_t qhead = 0;
@@ -623,6 +625,8 @@ struct Engine {
                             for (int j = -1; j <= 1; j += 2) {
                                 if (!vacant(v, ci + i, cj + j)) continue;
                                 ++stat_tests;
+                                if (trace) std::fprintf(stderr, "E pop %lld rec %d v %d i %d j %d child %lld acc %d cnt %d cell %d %d\n",
+                                    (long long)pops, r, v, i, j, (long long)child, (int)h_accept[child], h_count[child], h_cell[2*child], h_cell[2*child+1]);
                                 if (h_accept[child]) {
                                     fill_record(child);
                                     events.push_back((int32_t)child);
@@ -916,6 +920,66 @@ int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats) {
 }
 
 void mvs_stage_free(mvs_stage_result* res) { delete res; }
+
+int mvs_expand_candidates(mvs_ctx* ctx, int64_t n_parents, const double* pc, const double* pn,
+                          const double* pxy, int64_t n_jobs, const int32_t* job_parent,
+                          const int32_t* job_view, const int32_t* job_di, int cell_size,
+                          double scale, int wid, double min_ncc, double* X, double* nX,
+                          uint8_t* color, double* xy, uint64_t* mask, int32_t* count,
+                          uint8_t* accept) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (n_parents < 0 || n_jobs < 0 || cell_size < 1) return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
+    if (wid != 3 && wid != 5) return set_err(ctx, Fail{MVS_E_UNSUPPORTED, "expand supports wid 3 or 5"});
+    return guarded(ctx, [&]() {
+        for (int64_t k = 0; k < n_jobs; ++k)
+            if (job_parent[k] < 0 || job_parent[k] >= n_parents || job_view[k] < 0 ||
+                job_view[k] >= ctx->V || (job_di[k] != 1 && job_di[k] != -1))
+                throw Fail{MVS_E_ARG, "bad job"};
+        if (n_jobs == 0) return 0;
+        hipStream_t s = ctx->stream;
+        const int words = ctx->words();
+        const int64_t nr = n_parents + n_jobs;
+        DevBuf<double> c_, n_, xy_;
+        DevBuf<uint64_t> m_;
+        DevBuf<int32_t> R_, cnt_, cell_;
+        DevBuf<uint8_t> col_, acc_;
+        DevBuf<ChildJob> jobs_;
+        c_.alloc(nr * 3); n_.alloc(nr * 3); xy_.alloc(nr * 2); m_.alloc(nr * words); R_.alloc(nr);
+        cnt_.alloc(nr); cell_.alloc(nr * 2); col_.alloc(nr * 4); acc_.alloc(nr); jobs_.alloc(n_jobs);
+        std::vector<ChildJob> jobs(n_jobs);
+        for (int64_t k = 0; k < n_jobs; ++k)
+            jobs[k] = ChildJob{job_parent[k], (int16_t)job_view[k], (int16_t)job_di[k]};
+        HIPCHK(hipMemcpyAsync(c_.p, pc, n_parents * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(n_.p, pn, n_parents * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(xy_.p, pxy, n_parents * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(jobs_.p, jobs.data(), n_jobs * sizeof(ChildJob), hipMemcpyHostToDevice, s));
+        RecordsDev r;
+        r.c = c_.p; r.n = n_.p; r.xy = xy_.p; r.mask = m_.p; r.R = R_.p; r.count = cnt_.p;
+        r.color = col_.p; r.accept = acc_.p; r.cell = cell_.p;
+        ExpandArgs a{};
+        a.n = n_jobs;
+        a.first_out = n_parents;
+        a.jobs = jobs_.p;
+        a.cell_size = cell_size;
+        a.vlb = ctx->V > 2 ? 3 : 2;
+        a.dist_thr = 0.05 / scale;
+        a.thr = min_ncc;
+        a.exact_hits = ctx->d_exact.p;
+        if (mvs_launch_expand(&ctx->sc, r, &a, wid, s) != 0) throw Fail{MVS_E_HIP, "expand launch failed"};
+        std::vector<uint8_t> col4(n_jobs * 4);
+        HIPCHK(hipMemcpyAsync(X, c_.p + n_parents * 3, n_jobs * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(nX, n_.p + n_parents * 3, n_jobs * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(xy, xy_.p + n_parents * 2, n_jobs * 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(mask, m_.p + n_parents * words, n_jobs * words * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(count, cnt_.p + n_parents, n_jobs * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(accept, acc_.p + n_parents, n_jobs, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(col4.data(), col_.p + n_parents * 4, n_jobs * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int64_t k = 0; k < n_jobs; ++k)
+            for (int q = 0; q < 3; ++q) color[3 * k + q] = col4[4 * k + q];
+        return 0;
+    });
+}
 
 int mvs_rodrigues_roundtrip(const double* R, double* Rp) {
     if (!R || !Rp) return MVS_E_ARG;

@@ -156,7 +156,7 @@ def test_stage_vs_oracle(ctx, oracle_scene, seeds, cap):
     ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
                               cell_size=2, scale=10.0, wid=5, max_pops=cap)
     oini, oall, ost = oracle_scene.mvs_stage(seeds["track_off"], seeds["obs_view"],
-                                             seeds["obs_xy"], max_pops=cap)
+                                             seeds["obs_xy"], scale=10.0, max_pops=cap)
     assert st["pops"] == ost["pops"]
     assert st["tests"] == ost["tests"]
     assert st["queue_left"] == ost["queue_left"]
@@ -193,8 +193,8 @@ def test_stage_empty_and_ragged_tracks(ctx, oracle_scene, seeds):
             view.append(seeds["obs_view"][o]); xy.append(seeds["obs_xy"][o])
         off.append(len(view))
     args = (np.array(off, np.int64), np.array(view, np.int32), np.array(xy, np.float32))
-    ini, allp, st = ctx.stage(*args, max_pops=300)
-    oini, oall, ost = oracle_scene.mvs_stage(*args, max_pops=300)
+    ini, allp, st = ctx.stage(*args, scale=10.0, max_pops=300)
+    oini, oall, ost = oracle_scene.mvs_stage(*args, scale=10.0, max_pops=300)
     assert np.array_equal(ini, oini)
     assert np.array_equal(allp, oall)
 

@@ -47,7 +47,7 @@ def test_photo_test_bit_exact(oracle_scene, func_golden):
 def test_stage_bit_exact(oracle_scene, seeds, cap):
     g = stage_golden(cap)
     ini, allp, st = oracle_scene.mvs_stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
-                                           max_pops=cap)
+                                           scale=10.0, max_pops=cap)
     assert st["pops"] == cap
     assert np.array_equal(ini, g["initial_patches"])
     assert np.array_equal(allp, g["all_patches"])
