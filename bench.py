@@ -59,11 +59,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=100000)
     ap.add_argument("--secondary-wid", type=int, default=3)
+    ap.add_argument("--kernel", choices=["auto", "direct", "tiled"], default="auto",
+                    help="scoring kernel (MVS_SCORE_KERNEL)")
     a = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
+    if a.kernel != "auto":
+        os.environ["MVS_SCORE_KERNEL"] = a.kernel
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -86,7 +90,9 @@ def main():
     count = torch.empty(n, dtype=torch.int32, device=dev)
     avg = torch.empty(n, dtype=torch.float64, device=dev)
     vlb = 3 if V > 2 else 2
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)          # the scoring kernels run on THIS stream
+    torch.cuda.synchronize()
+    torch.cuda.set_stream(stream)
     gathered = {"n": 0}
 
     def step(wid, evs=None):
@@ -202,7 +208,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM,
                          "traffic": traffic,
-                         "kernel": "k_score<5,1>" if a.wid == 5 else f"k_score<{a.wid},1>",
+                         "kernel": a.kernel,
                          "kernel_ms": kms, "bytes_per_candidate": B},
             "cpu_baseline": cpu,
             "accepted_per_sweep": accepted,

@@ -66,7 +66,9 @@ int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp);
  * Host pointers; synchronous. wid in 1..5. */
 int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int wid,
               double min_ncc, double* xy, uint64_t* mask, int32_t* count, double* avg);
-/* Same on device pointers (e.g. torch tensor data_ptr()), stream-ordered. */
+/* Same on device pointers (e.g. torch tensor data_ptr()), stream-ordered.
+ * d_avg may be NULL when avg_ncc_score is not needed (it only feeds the
+ * disabled filter_out_outlier, MVS2.py:281). */
 int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
                      double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
                      double* d_avg, void* stream);

@@ -190,7 +190,8 @@ class MvsContext:
         n = int(ref.numel()) if hasattr(ref, "numel") else int(len(ref))
         ptr = (lambda x: x.data_ptr()) if hasattr(ref, "data_ptr") else (lambda x: int(x))
         rc = load().mvs_score_device(self._h, n, ptr(c), ptr(ref), int(wid), float(min_ncc),
-                                     ptr(xy), ptr(mask), ptr(count), ptr(avg),
+                                     ptr(xy), ptr(mask), ptr(count),
+                                     ptr(avg) if avg is not None else None,
                                      stream if stream is not None else None)
         check(rc, self._h, "mvs_score_device")
 

@@ -279,6 +279,11 @@ struct mvs_ctx {
     DevBuf<double> s_c, s_xy, s_avg;
     DevBuf<int32_t> s_ref, s_count;
     DevBuf<uint64_t> s_mask;
+    // tiled scorer scratch
+    int ntx = 0, nty = 0;
+    DevBuf<int32_t> t_tiles, t_cand;
+    int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
+    int variant = 0;       // tiled-kernel variant (env MVS_VARIANT), see mvs_kernels.hip
     std::string err;
     int words() const { return (V + 63) / 64; }
 };
@@ -351,6 +356,27 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
     a.count = d_count;
     a.avg = d_avg;
     a.exact_hits = ctx->d_exact.p;
+    const bool tiled = ctx->V <= 64 && (ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048));
+    if (tiled) {
+        const int ntiles = ctx->ntx * ctx->nty;
+        ctx->t_tiles.ensure((size_t)3 * (ntiles + 1));
+        ctx->t_cand.ensure((size_t)5 * n);
+        TiledArgs t{};
+        t.ntx = ctx->ntx;
+        t.nty = ctx->nty;
+        t.ntiles = ntiles;
+        t.chunk = 512;
+        t.tile_count = ctx->t_tiles.p;
+        t.tile_off = ctx->t_tiles.p + (ntiles + 1);
+        t.item_off = ctx->t_tiles.p + 2 * (ntiles + 1);
+        t.cand_key = ctx->t_cand.p;
+        t.cand_rank = ctx->t_cand.p + n;
+        t.cand_pk = ctx->t_cand.p + 2 * n;
+        t.sorted = (int2*)(ctx->t_cand.p + 3 * n);
+        if (mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, ctx->variant, s) != 0)
+            throw Fail{MVS_E_HIP, "tiled score launch failed"};
+        return;
+    }
     if (mvs_launch_score(&ctx->sc, &a, wid, s) != 0) throw Fail{MVS_E_HIP, "score launch failed"};
 }
 
@@ -783,6 +809,12 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
         ctx->sc.stack = ctx->d_stack.p;
         ctx->sc.rgb = ctx->d_rgb.p;
         ctx->sc.cams = ctx->d_cams.p;
+        mvs_tiled_geometry(W, H, &ctx->ntx, &ctx->nty);
+        if (const char* vv = std::getenv("MVS_VARIANT")) ctx->variant = std::atoi(vv);
+        if (const char* km = std::getenv("MVS_SCORE_KERNEL")) {
+            if (!std::strcmp(km, "direct")) ctx->kernel_mode = 1;
+            else if (!std::strcmp(km, "tiled")) ctx->kernel_mode = 2;
+        }
         return 0;
     });
     if (rc != 0) {

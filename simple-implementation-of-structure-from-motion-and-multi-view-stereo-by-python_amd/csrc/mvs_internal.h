@@ -47,6 +47,22 @@ struct ScoreArgs {
     int32_t* exact_hits;  // 1 counter: lanes that took the exact (numpy-order) path
 };
 
+// Scratch of the tiled scorer (device pointers, sized by the host).
+//   tile_count[ntiles+1], tile_off[ntiles+1], item_off[ntiles+1], n_items[1]
+//   cand_key[n]  = tile (or -1 if the window is invalid), cand_rank[n],
+//   cand_pk[n]   = q | r << 11 | R << 22, sorted[n] = {id, pk} grouped by tile
+struct TiledArgs {
+    int ntx, nty, ntiles;
+    int chunk;                 // candidates per work item
+    int32_t* tile_count;
+    int32_t* tile_off;
+    int32_t* item_off;
+    int32_t* cand_key;
+    int32_t* cand_rank;
+    int32_t* cand_pk;
+    int2* sorted;
+};
+
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).
 struct ChildJob {
     int32_t parent;
@@ -82,6 +98,10 @@ extern "C" {
 int mvs_launch_build_stack(const uint8_t* d_rgb, uint8_t* d_stack, int V, int H, int W, int Wq,
                            hipStream_t s);
 int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s);
+// Tile geometry of the tiled scorer for a W x H image (so the host can size scratch).
+void mvs_tiled_geometry(int W, int H, int* ntx, int* nty);
+int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
+                           int variant, hipStream_t s);
 int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, int wid,
                       hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,

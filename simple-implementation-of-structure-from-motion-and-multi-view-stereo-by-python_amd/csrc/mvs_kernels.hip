@@ -16,6 +16,8 @@
 // Geometry is binary64 in the reference's order; this file must be compiled
 // with -ffp-contract=off (products that numpy/OpenBLAS fuse are written as
 // fma() explicitly).
+#include <algorithm>
+
 #include "mvs_internal.h"
 
 #define DEV __device__ __forceinline__
@@ -94,7 +96,7 @@ DEV double exact_ncc_generic(FA&& A, FB&& B, int n) {
 }
 
 template <int WID>
-__device__ __noinline__ double exact_ncc_stack(const SceneDev sc, int R, int v, int q, int r) {
+__device__ __forceinline__ double exact_ncc_stack(const SceneDev sc, int R, int v, int q, int r) {
     constexpr int NB = 2 * WID + 1;
     auto A = [&](int i) -> int { return stack_px(sc, R, r - WID + i / NB, q - WID + i % NB); };
     auto B = [&](int i) -> int { return stack_px(sc, v, r - WID + i / NB, q - WID + i % NB); };
@@ -107,41 +109,131 @@ DEV double wave_sum(double x) {
     return x;
 }
 
+// One window row of every view of this lane: align, broadcast the reference
+// view's words, accumulate S_ab (dot4), S_bb (dot4), S_b (sad).
+template <int NS, int NW, int ND, uint32_t LASTMASK, class Fetch>
+DEV void wave_row(Fetch&& fetch, int row, int o, int V, int Rs, int Rl, int lane, uint32_t* Sb,
+                  uint32_t* Sbb, uint32_t* Sab) {
+    uint32_t w[NS][NW];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int v = lane + 64 * s;
+        uint32_t d[ND];
+        if (NS == 1 || v < V) {
+#pragma unroll
+            for (int j = 0; j < ND; ++j) d[j] = fetch(s, row, j);
+        } else {
+#pragma unroll
+            for (int j = 0; j < ND; ++j) d[j] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) w[s][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], o);
+        w[s][NW - 1] &= LASTMASK;
+    }
+    uint32_t a[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        uint32_t src = w[0][j];
+#pragma unroll
+        for (int s = 1; s < NS; ++s) src = (Rs == s) ? w[s][j] : src;
+        a[j] = __builtin_amdgcn_readlane(src, Rl);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            Sab[s] = __builtin_amdgcn_udot4(a[j], w[s][j], Sab[s], false);
+            Sbb[s] = __builtin_amdgcn_udot4(w[s][j], w[s][j], Sbb[s], false);
+            Sb[s] = __builtin_amdgcn_sad_u8(w[s][j], 0u, Sb[s]);
+        }
+    }
+}
+
 // One wave scores one candidate whose window sits at (q, r) of every view
 // (the reference samples all views at view R's pixel, MVS2.py:68).
-// Lane l handles views l, l+64, ... (NS slots).  Returns nothing; lane 0 of
-// the wave writes mask/count/avg.
-template <int WID, int NS>
-DEV void wave_score(const SceneDev& sc, int R, int q, int r, double thr, uint64_t* mask_out,
-                    int32_t* count_out, double* avg_out, int32_t* exact_hits) {
+// Lane l handles views l, l+64, ... (NS slots).  fetch(s, row, j) returns the
+// j-th dword (4 pixels of this lane's view of slot s) of window row `row`,
+// counted from the quad holding column q - WID; o = (q - WID) & 3.
+// Lane 0 of the wave writes mask/count/avg.
+// Variants (A/B-able at run time, see mvs_launch_score_tiled):
+//   EPI 0: decision from the binary64 closed form (guard 1e-9 -> numpy order)
+//   EPI 1: decision from a binary32 closed form (|err| < 4e-7; guard 1e-5 ->
+//          binary64 -> guard 1e-9 -> numpy order); binary64 only for lanes in
+//          the guard and, when avg is wanted, for passing lanes
+//   REF 0: reference-view words broadcast with v_readlane
+//   REF 1: reference-view words re-read by every lane (same LDS address = broadcast)
+template <int WID, int NS, bool UNROLL = false, int EPI = 0, int REF = 0, class Fetch,
+          class FetchRef>
+DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fetch&& fetch,
+                         FetchRef&& fref, uint64_t* mask_out, int32_t* count_out,
+                         double* avg_out, int32_t* exact_hits) {
     constexpr int NB = 2 * WID + 1;
     constexpr int NPX = NB * NB;
     constexpr int NW = (NB + 3) / 4;
     constexpr int ND = NW + 1;
     constexpr uint32_t LASTMASK = (NB % 4 == 0) ? 0xffffffffu : ((1u << (8 * (NB % 4))) - 1u);
     const int lane = threadIdx.x & 63;
-    const int q0 = q - WID;
-    const int k0 = q0 >> 2, o = q0 & 3;
+    const int o = (q - WID) & 3;
     const int V = sc.V;
-    const int64_t vstride = (int64_t)V * 4;
-    const uint8_t* p0 = sc.stack + (int64_t)(r - WID) * sc.row_bytes + (int64_t)k0 * vstride;
     const int Rs = R >> 6, Rl = R & 63;
 
     uint32_t Sb[NS], Sbb[NS], Sab[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) Sb[s] = Sbb[s] = Sab[s] = 0;
 
-    for (int row = 0; row < NB; ++row) {
-        const uint8_t* prow = p0 + (int64_t)row * sc.row_bytes;
+    if constexpr (UNROLL) {
+        // LDS-resident rows: issue every read of the window first, then run
+        // the dot products on NW independent accumulator chains.
+        static_assert(NS == 1, "unrolled path is single-slot");
+        uint32_t d[NB][ND];
+#pragma unroll
+        for (int row = 0; row < NB; ++row)
+#pragma unroll
+            for (int j = 0; j < ND; ++j) d[row][j] = fetch(0, row, j);
+        uint32_t ab[NW], bb[NW], b1[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) ab[j] = bb[j] = b1[j] = 0;
+#pragma unroll
+        for (int row = 0; row < NB; ++row) {
+            uint32_t w[NW], a[NW];
+#pragma unroll
+            for (int j = 0; j < NW; ++j) w[j] = __builtin_amdgcn_alignbyte(d[row][j + 1], d[row][j], o);
+            w[NW - 1] &= LASTMASK;
+            if constexpr (REF == 0) {
+#pragma unroll
+                for (int j = 0; j < NW; ++j) a[j] = __builtin_amdgcn_readlane(w[j], Rl);
+            } else {
+                uint32_t e[ND];
+#pragma unroll
+                for (int j = 0; j < ND; ++j) e[j] = fref(row, j);
+#pragma unroll
+                for (int j = 0; j < NW; ++j) a[j] = __builtin_amdgcn_alignbyte(e[j + 1], e[j], o);
+                a[NW - 1] &= LASTMASK;
+            }
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                ab[j] = __builtin_amdgcn_udot4(a[j], w[j], ab[j], false);
+                bb[j] = __builtin_amdgcn_udot4(w[j], w[j], bb[j], false);
+                b1[j] = __builtin_amdgcn_sad_u8(w[j], 0u, b1[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            Sab[0] += ab[j];
+            Sbb[0] += bb[j];
+            Sb[0] += b1[j];
+        }
+    }
+#pragma unroll 1
+    for (int row = 0; row < (UNROLL ? 0 : NB); ++row) {
         uint32_t w[NS][NW];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const int v = lane + 64 * s;
             uint32_t d[ND];
-            if (v < V) {
-                const uint8_t* pv = prow + v * 4;
+            if (NS == 1 || v < V) {
 #pragma unroll
-                for (int j = 0; j < ND; ++j) d[j] = *(const uint32_t*)(pv + j * vstride);
+                for (int j = 0; j < ND; ++j) d[j] = fetch(s, row, j);
             } else {
 #pragma unroll
                 for (int j = 0; j < ND; ++j) d[j] = 0;
@@ -189,25 +281,66 @@ DEV void wave_score(const SceneDev& sc, int R, int q, int r, double thr, uint64_
         const int64_t num = (int64_t)NPX * (int64_t)Sab[s] - Sa * sb;
         bool pass = false;
         double ncc = 0.0;
-        if (v < V && v != R && da > 0 && db > 0) {   // da or db == 0: ctNcc is nan -> rejected
-            ncc = (double)((int64_t)NPX * num) /
-                  ((double)(NPX - 1) * sqrt((double)da * (double)db));
-            if (fabs(ncc - thr) <= kGuard) {
-                ncc = exact_ncc_stack<WID>(sc, R, v, q, r);
-                atomicAdd(exact_hits, 1);
+        const bool live = v < V && v != R && da > 0 && db > 0;   // da/db == 0: ctNcc nan -> reject
+        auto ncc64 = [&]() {
+            return (double)((int64_t)NPX * num) / ((double)(NPX - 1) * sqrt((double)da * (double)db));
+        };
+        if constexpr (EPI == 0) {
+            if (live) {
+                ncc = ncc64();
+                if (fabs(ncc - thr) <= kGuard) {
+                    ncc = exact_ncc_stack<WID>(sc, R, v, q, r);
+                    atomicAdd(exact_hits, 1);
+                }
+                pass = ncc > thr;
             }
-            pass = ncc > thr;
+        } else {
+            if (live) {
+                const float n32 = (float)((int64_t)NPX * num) /
+                                  ((float)(NPX - 1) * sqrtf((float)da * (float)db));
+                const float thr32 = (float)thr;
+                if (fabsf(n32 - thr32) <= 1e-5f) {
+                    ncc = ncc64();
+                    if (fabs(ncc - thr) <= kGuard) {
+                        ncc = exact_ncc_stack<WID>(sc, R, v, q, r);
+                        atomicAdd(exact_hits, 1);
+                    }
+                    pass = ncc > thr;
+                } else {
+                    pass = n32 > thr32;
+                    if (pass && avg_out) ncc = ncc64();
+                }
+            }
         }
         const uint64_t m = __ballot(pass);
         if (lane == 0) mask_out[s] = m;
         cnt += __popcll(m);
         acc += pass ? ncc : 0.0;
     }
+    if (EPI == 1 && !avg_out) {
+        if (lane == 0) *count_out = cnt;
+        return;
+    }
     const double tot = wave_sum(acc);
     if (lane == 0) {
         *count_out = cnt;
         if (avg_out) *avg_out = cnt > 0 ? tot / cnt : 0.0;
     }
+}
+
+// Direct variant: window rows gathered straight from the HBM-resident stack.
+template <int WID, int NS>
+DEV void wave_score(const SceneDev& sc, int R, int q, int r, double thr, uint64_t* mask_out,
+                    int32_t* count_out, double* avg_out, int32_t* exact_hits) {
+    const int lane = threadIdx.x & 63;
+    const int k0 = (q - WID) >> 2;
+    const int64_t vstride = (int64_t)sc.V * 4;
+    const uint8_t* p0 = sc.stack + (int64_t)(r - WID) * sc.row_bytes + (int64_t)k0 * vstride;
+    auto fetch = [&](int s, int row, int j) -> uint32_t {
+        return *(const uint32_t*)(p0 + (int64_t)row * sc.row_bytes + j * vstride + (lane + 64 * s) * 4);
+    };
+    auto fref = [&](int, int) -> uint32_t { return 0u; };
+    wave_score_core<WID, NS>(sc, R, q, r, thr, fetch, fref, mask_out, count_out, avg_out, exact_hits);
 }
 
 template <int NS>
@@ -262,13 +395,186 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
     if (lane == 0) { a.xy[2 * cand] = px; a.xy[2 * cand + 1] = py; }
     int q, r;
     if (!window_ok(sc, px, py, WID, &q, &r)) {
-        wave_score_empty<NS>(a.mask + cand * words, a.count + cand, a.avg + cand);
+        wave_score_empty<NS>(a.mask + cand * words, a.count + cand, a.avg ? a.avg + cand : nullptr);
         return;
     }
     q = __builtin_amdgcn_readfirstlane(q);
     r = __builtin_amdgcn_readfirstlane(r);
-    wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * words, a.count + cand, a.avg + cand,
-                        a.exact_hits);
+    wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * words, a.count + cand,
+                        a.avg ? a.avg + cand : nullptr, a.exact_hits);
+}
+
+// ---------------------------------------------------------------------------
+// Tiled scorer: candidates binned by the TWxTH pixel tile of their window
+// centre; a workgroup stages the tile's window region of ALL views in LDS
+// (a straight copy of the stack's [row][quad][view] layout) and its waves
+// score the tile's candidates from LDS.
+// ---------------------------------------------------------------------------
+constexpr int kTW = 16, kTH = 8, kChunk = 512, kTiledBlocks = 2048;
+
+template <int WID>
+struct TileGeom {
+    static constexpr int NB = 2 * WID + 1;
+    static constexpr int NW = (NB + 3) / 4;
+    static constexpr int KQ0 = -((WID + 3) / 4);                 // first quad, relative to x0/4
+    static constexpr int KQL = ((kTW - 1 - WID) >> 2) + NW;        // last quad read, relative
+    static constexpr int NQ = KQL - KQ0 + 1;
+    static constexpr int ROWS = kTH + 2 * WID;
+};
+
+// k_bin: project every candidate (FP64, reference order), test its window,
+// and rank it inside its tile.  Ranks come from an LDS histogram per block
+// (one global atomic per non-empty (block, tile) pair), not from a global
+// atomic per candidate.
+constexpr int kBinBlock = 1024, kBinPer = 8;
+
+__global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
+                                                   const TiledArgs t, int wid) {
+    extern __shared__ int32_t hist[];      // [ntiles] local counts, then global bases
+    const int words = (sc.V + 63) >> 6;
+    for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
+    int tl[kBinPer], lr[kBinPer];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        tl[k] = -1;
+        if (i >= a.n) continue;
+        const int R = a.ref[i];
+        const double c[3] = {a.c[3 * i], a.c[3 * i + 1], a.c[3 * i + 2]};
+        double px, py;
+        project(sc.cams[R], c, px, py);
+        a.xy[2 * i] = px;
+        a.xy[2 * i + 1] = py;
+        int q, r;
+        if (!window_ok(sc, px, py, wid, &q, &r)) {
+            for (int w = 0; w < words; ++w) a.mask[i * words + w] = 0;
+            a.count[i] = 0;
+            if (a.avg) a.avg[i] = 0.0;
+            t.cand_key[i] = -1;
+            continue;
+        }
+        const int tile = (r / kTH) * t.ntx + (q / kTW);
+        tl[k] = tile;
+        t.cand_pk[i] = q | (r << 11) | (R << 22);
+        lr[k] = atomicAdd(&hist[tile], 1);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) {
+        const int c = hist[b];
+        hist[b] = c ? atomicAdd(&t.tile_count[b], c) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        if (tl[k] < 0) continue;
+        t.cand_key[i] = tl[k];
+        t.cand_rank[i] = hist[tl[k]] + lr[k];
+    }
+}
+
+// Exclusive scans of tile counts and work items (one workgroup).
+__global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
+    __shared__ int32_t part_c[1024], part_i[1024];
+    const int tid = threadIdx.x;
+    const int per = (t.ntiles + 1023) / 1024;
+    const int b = tid * per, e = min(b + per, t.ntiles);
+    int32_t sc = 0, si = 0;
+    for (int k = b; k < e; ++k) {
+        const int c = t.tile_count[k];
+        sc += c;
+        si += (c + t.chunk - 1) / t.chunk;
+    }
+    part_c[tid] = sc;
+    part_i[tid] = si;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        int32_t vc = tid >= off ? part_c[tid - off] : 0;
+        int32_t vi = tid >= off ? part_i[tid - off] : 0;
+        __syncthreads();
+        part_c[tid] += vc;
+        part_i[tid] += vi;
+        __syncthreads();
+    }
+    int32_t rc = tid ? part_c[tid - 1] : 0, ri = tid ? part_i[tid - 1] : 0;
+    for (int k = b; k < e; ++k) {
+        t.tile_off[k] = rc;
+        t.item_off[k] = ri;
+        const int c = t.tile_count[k];
+        rc += c;
+        ri += (c + t.chunk - 1) / t.chunk;
+    }
+    if (tid == 1023) {
+        t.tile_off[t.ntiles] = part_c[1023];
+        t.item_off[t.ntiles] = part_i[1023];
+    }
+}
+
+__global__ void k_scatter(const ScoreArgs a, const TiledArgs t) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int tile = t.cand_key[i];
+        if (tile >= 0) t.sorted[t.tile_off[tile] + t.cand_rank[i]] = make_int2((int32_t)i, t.cand_pk[i]);
+    }
+}
+
+// LDS image of a tile region: [row][quad][64 view slots] dwords, so every
+// window dword of lane v sits at a compile-time offset from one base address
+// (ds_read2st64_b32 pairs), and the 64 lanes of a read hit 64 banks.
+template <int WID, int EPI, int REF>
+__global__ __launch_bounds__(256) void k_score_tiled(const SceneDev sc, const ScoreArgs a,
+                                                     const TiledArgs t) {
+    using G = TileGeom<WID>;
+    constexpr int QS = 64;                 // dwords per (row, quad)
+    constexpr int RS = G::NQ * QS;         // dwords per region row
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int V = sc.V;                    // <= 64
+    const int n_items = t.item_off[t.ntiles];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+        int lo = 0, hi = t.ntiles;         // tile = last k with item_off[k] <= item
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t.item_off[mid] <= item) lo = mid; else hi = mid;
+        }
+        const int tile = lo;
+        const int chunk = item - t.item_off[tile];
+        const int cb = t.tile_off[tile] + chunk * t.chunk;
+        const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int y0 = ty * kTH - WID;                 // first region row
+        const int kq0 = tx * (kTW / 4) + G::KQ0;       // first region quad
+        // stage: wave w copies (row, quad) pairs w, w+4, ...; lane = view
+        for (int pq = wave; pq < G::ROWS * G::NQ; pq += 4) {
+            const int ry = pq / G::NQ, kq = pq - ry * G::NQ;
+            const int y = y0 + ry, gq = kq0 + kq;
+            uint32_t val = 0;
+            if (lane < V && y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                val = *(const uint32_t*)(sc.stack + (int64_t)y * sc.row_bytes + (int64_t)gq * V * 4 + lane * 4);
+            lds[pq * QS + lane] = val;
+        }
+        __syncthreads();
+        int2 nxt = cb + wave < ce ? t.sorted[cb + wave] : make_int2(0, 0);
+        for (int j = cb + wave; j < ce; j += 4) {
+            const int2 cur = nxt;
+            if (j + 4 < ce) nxt = t.sorted[j + 4];
+            const int i = __builtin_amdgcn_readfirstlane(cur.x);
+            const int pk = __builtin_amdgcn_readfirstlane(cur.y);
+            const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
+            const int ry0 = r - WID - y0;
+            const int k0 = ((q - WID) >> 2) - kq0;
+            const uint32_t* basep = lds + ry0 * RS + k0 * QS + lane;
+            auto fetch = [&](int, int row, int jj) -> uint32_t { return basep[row * RS + jj * QS]; };
+            const uint32_t* refp = basep - lane + R;
+            auto fref = [&](int row, int jj) -> uint32_t { return refp[row * RS + jj * QS]; };
+            wave_score_core<WID, 1, true, EPI, REF>(sc, R, q, r, a.thr, fetch, fref, a.mask + i,
+                                                    a.count + i, a.avg ? a.avg + i : nullptr,
+                                                    a.exact_hits);
+        }
+        __syncthreads();
+    }
 }
 
 DEV double dot3(const double* a, const double* b) {
@@ -412,6 +718,28 @@ int launch_score_w(const SceneDev* sc, const ScoreArgs* a, hipStream_t s) {
 }
 
 template <int WID>
+int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int variant,
+                         hipStream_t s) {
+    using G = TileGeom<WID>;
+    if (a->n == 0) return 0;
+    if (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 1), s) != hipSuccess) return -1;
+    const int64_t per_block = (int64_t)kBinBlock * kBinPer;
+    const int nbin = (int)((a->n + per_block - 1) / per_block);
+    hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, *t);
+    const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
+    const size_t lds = (size_t)G::ROWS * G::NQ * 64 * 4;
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((k_score_tiled<WID, 0, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+        case 1: hipLaunchKernelGGL((k_score_tiled<WID, 1, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+        case 2: hipLaunchKernelGGL((k_score_tiled<WID, 0, 1>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+        default: hipLaunchKernelGGL((k_score_tiled<WID, 1, 1>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int WID>
 int launch_expand_w(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, hipStream_t s) {
     const int64_t blocks = (a->n + 3) / 4;
     if (blocks == 0) return 0;
@@ -441,6 +769,24 @@ extern "C" int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid,
         case 3: return launch_score_w<3>(sc, a, s);
         case 4: return launch_score_w<4>(sc, a, s);
         case 5: return launch_score_w<5>(sc, a, s);
+        default: return -2;
+    }
+}
+
+extern "C" void mvs_tiled_geometry(int W, int H, int* ntx, int* nty) {
+    *ntx = (W + kTW - 1) / kTW;
+    *nty = (H + kTH - 1) / kTH;
+}
+
+extern "C" int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t,
+                                      int wid, int variant, hipStream_t s) {
+    if (sc->V > 64) return -3;
+    switch (wid) {
+        case 1: return launch_score_tiled_w<1>(sc, a, t, variant, s);
+        case 2: return launch_score_tiled_w<2>(sc, a, t, variant, s);
+        case 3: return launch_score_tiled_w<3>(sc, a, t, variant, s);
+        case 4: return launch_score_tiled_w<4>(sc, a, t, variant, s);
+        case 5: return launch_score_tiled_w<5>(sc, a, t, variant, s);
         default: return -2;
     }
 }

@@ -23,6 +23,24 @@ def ctx(pkg, dino):
     c.close()
 
 
+@pytest.fixture(scope="module", params=["direct", "tiled"])
+def kctx(request, pkg, dino):
+    """A context forced onto one scoring kernel (MVS_SCORE_KERNEL)."""
+    import os
+    rgb, K, R, t = dino
+    old = os.environ.get("MVS_SCORE_KERNEL")
+    os.environ["MVS_SCORE_KERNEL"] = request.param
+    try:
+        c = pkg.MvsContext(rgb, K, R, t, device=0)
+    finally:
+        if old is None:
+            del os.environ["MVS_SCORE_KERNEL"]
+        else:
+            os.environ["MVS_SCORE_KERNEL"] = old
+    yield c
+    c.close()
+
+
 def test_rproj_matches_oracle(ctx, oracle_scene):
     assert np.array_equal(ctx.rproj().reshape(-1, 9), oracle_scene.Rp)
 
@@ -38,11 +56,11 @@ def test_photo_test_vs_reference_golden(ctx, func_golden):
         np.testing.assert_allclose(avg, f["pt_avg"][sel], rtol=0, atol=AVG_TOL)
 
 
-@pytest.mark.parametrize("wid,thr", [(5, 0.7), (5, 0.4), (3, 0.7), (1, 0.5)])
-def test_score_vs_oracle_bench_batch(ctx, oracle_scene, dino, wid, thr):
+@pytest.mark.parametrize("wid,thr", [(5, 0.7), (5, 0.4), (3, 0.7), (1, 0.5), (2, 0.6), (4, 0.7)])
+def test_score_vs_oracle_bench_batch(kctx, oracle_scene, dino, wid, thr):
     rgb, K, R, t = dino
     c, ref = bench_candidates(6000, K, R, t, seed=wid)
-    xy, mask, count, avg = ctx.score(c, ref, thr, wid)
+    xy, mask, count, avg = kctx.score(c, ref, thr, wid)
     oxy, omask, ocount, oavg = oracle_scene.score_batch(c, ref, thr, wid, nthreads=8)
     assert np.array_equal(xy, oxy)
     assert np.array_equal(mask, omask)
@@ -51,7 +69,7 @@ def test_score_vs_oracle_bench_batch(ctx, oracle_scene, dino, wid, thr):
     assert count.sum() > 0
 
 
-def test_score_edge_candidates(ctx, oracle_scene, dino):
+def test_score_edge_candidates(kctx, oracle_scene, dino):
     """Windows touching every bound of HarrisFeatures.py:128, points behind the
     camera, at the camera centre (z = 0 -> OpenCV's 1/z guard) and far away."""
     rgb, K, R, t = dino
@@ -69,8 +87,28 @@ def test_score_edge_candidates(ctx, oracle_scene, dino):
         cs.append(O - 0.5 * (R[v].T @ np.array([0, 0, 1.0]))); refs.append(v)      # behind
         cs.append(O + 1e6 * (R[v].T @ np.array([0.1, 0.1, 1.0]))); refs.append(v)  # far
     c, ref = np.array(cs), np.array(refs, np.int32)
-    got = ctx.score(c, ref, 0.7, 5)
-    exp = oracle_scene.score_batch(c, ref, 0.7, 5)
+    for rep in (1, 8):   # x8: enough candidates for the auto mode to tile too
+        cc, rr = np.tile(c, (rep, 1)), np.tile(ref, rep)
+        got = kctx.score(cc, rr, 0.7, 5)
+        exp = oracle_scene.score_batch(cc, rr, 0.7, 5)
+        for g, e in zip(got[:3], exp[:3]):
+            assert np.array_equal(g, e)
+
+
+def test_score_dense_tile(kctx, oracle_scene, dino):
+    """Many candidates in one pixel tile (several LDS work items per tile)."""
+    rgb, K, R, t = dino
+    rng = np.random.default_rng(9)
+    n = 5000
+    ref = rng.integers(0, 48, n).astype(np.int32)
+    x = 300 + rng.random(n) * 16
+    y = 200 + rng.random(n) * 8
+    z = rng.uniform(0.6, 0.72, n)
+    Kinv = np.linalg.inv(K)
+    c = np.array([R[v].T @ (zz * (Kinv[v] @ np.array([xx, yy, 1.0])) - t[v].ravel())
+                  for v, xx, yy, zz in zip(ref, x, y, z)])
+    got = kctx.score(c, ref, 0.5, 5)
+    exp = oracle_scene.score_batch(c, ref, 0.5, 5)
     for g, e in zip(got[:3], exp[:3]):
         assert np.array_equal(g, e)
 
