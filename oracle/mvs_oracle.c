@@ -341,6 +341,23 @@ int or_photo_test(const or_scene *S, const double *c, int R, double thr, int wid
     return cnt;
 }
 
+/* Per-view ctNcc values of one candidate (nan where the reference computes
+ * nan, -inf for idx == R or an invalid window): lets tests put a threshold
+ * exactly on a reference value. */
+void or_photo_ncc(const or_scene *S, const double *c, int R, int wid, double *ncc_out) {
+    int n = (2 * wid + 1) * (2 * wid + 1);
+    uint8_t base[1024], des[1024];
+    double p[2];
+    or_project(S->K + 9 * R, S->Rp + 9 * R, S->t + 3 * R, c, p);
+    int base_ok = or_get_desc(S->gray + (int64_t)R * S->H * S->W, S->H, S->W, p[1], p[0], wid, base);
+    for (int idx = 0; idx < S->V; idx++) {
+        ncc_out[idx] = -INFINITY;
+        if (idx == R || !base_ok) continue;
+        if (or_get_desc(S->gray + (int64_t)idx * S->H * S->W, S->H, S->W, p[1], p[0], wid, des))
+            ncc_out[idx] = or_ctncc(base, des, n);
+    }
+}
+
 /* Batched photo test: the CPU baseline and the GPU parity checker.  mask has
  * ceil(V/64) words per candidate. */
 void or_score_batch(const or_scene *S, int64_t n, const double *c, const int32_t *ref, double thr,

@@ -53,11 +53,12 @@ SIGNATURES = [
 _lib = None
 
 
-def load(path=LIB_PATH):
+def load(path=None):
     """Load libmvs_amd.so; raises RuntimeError if it is absent (no fallback)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("MVS_LIB", LIB_PATH)
     if not os.path.exists(path):
         raise RuntimeError(
             f"libmvs_amd.so not found at {path}: build it with __graft_entry__.build() "

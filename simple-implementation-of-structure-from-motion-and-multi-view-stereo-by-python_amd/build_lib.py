@@ -11,6 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmvs_amd.so")
+STAMPS_LIB = os.path.join(HERE, "libmvs_amd_stamps.so")   # diagnostic build (-DMVS_STAMPS)
 SOURCES = ["mvs_kernels.hip", "mvs_engine.cpp"]
 HEADERS = ["mvs_internal.h", os.path.join("..", "..", "include", "mvs_amd.h")]
 ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
@@ -23,19 +24,22 @@ def needs_build():
     return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
+def build(force=False, verbose=False, stamps=False):
+    out = STAMPS_LIB if stamps else LIB
+    if not stamps and not force and not needs_build():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
-           "-o", LIB + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
+           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
+    if stamps:
+        cmd.append("-DMVS_STAMPS")
+    cmd += ["-o", out + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv))

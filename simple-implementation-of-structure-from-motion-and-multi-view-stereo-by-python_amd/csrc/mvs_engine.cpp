@@ -271,7 +271,8 @@ struct mvs_ctx {
     std::vector<CamDev> cams;
     std::vector<double> K;   // V*9 as given (getProjectionMatrix uses all of K)
     std::vector<uint8_t> h_rgb;
-    DevBuf<uint8_t> d_rgb, d_stack;
+    DevBuf<uint8_t> d_rgb, d_stack, d_gv;
+    DevBuf<uint2> d_mom[MVS_MAX_WID + 1];
     DevBuf<CamDev> d_cams;
     DevBuf<int32_t> d_exact;
     SceneDev sc{};
@@ -284,6 +285,7 @@ struct mvs_ctx {
     DevBuf<int32_t> t_tiles, t_cand;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
     int variant = 0;       // tiled-kernel variant (env MVS_VARIANT), see mvs_kernels.hip
+    int chunk3 = 256;      // candidates per work item of the v3 tiled kernel (env MVS_TILE_CHUNK)
     std::string err;
     int words() const { return (V + 63) / 64; }
 };
@@ -357,6 +359,14 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
     a.avg = d_avg;
     a.exact_hits = ctx->d_exact.p;
     const bool tiled = ctx->V <= 64 && (ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048));
+    if (tiled && (ctx->variant == 4 || ctx->variant == 5 || ctx->variant == 0) && (ctx->V & 3) == 0 &&
+        !ctx->sc.mom[wid]) {
+        // scene moments for this window size: built once, reused by every batch
+        ctx->d_mom[wid].alloc((size_t)ctx->H * ctx->W * ctx->V);
+        if (mvs_launch_build_moments(&ctx->sc, wid, ctx->d_mom[wid].p, s) != 0)
+            throw Fail{MVS_E_HIP, "moments launch failed"};
+        ctx->sc.mom[wid] = ctx->d_mom[wid].p;
+    }
     if (tiled) {
         const int ntiles = ctx->ntx * ctx->nty;
         ctx->t_tiles.ensure((size_t)3 * (ntiles + 1));
@@ -365,7 +375,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.ntx = ctx->ntx;
         t.nty = ctx->nty;
         t.ntiles = ntiles;
-        t.chunk = 512;
+        t.chunk = (ctx->variant == 0 || ctx->variant >= 4) ? ctx->chunk3 : 512;
         t.tile_count = ctx->t_tiles.p;
         t.tile_off = ctx->t_tiles.p + (ntiles + 1);
         t.item_off = ctx->t_tiles.p + 2 * (ntiles + 1);
@@ -809,8 +819,16 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
         ctx->sc.stack = ctx->d_stack.p;
         ctx->sc.rgb = ctx->d_rgb.p;
         ctx->sc.cams = ctx->d_cams.p;
+        ctx->sc.Wp = ((W + 3) & ~3) + 16;
+        ctx->d_gv.alloc((size_t)V * H * ctx->sc.Wp + 64);
+        if (mvs_launch_build_gv(ctx->d_stack.p, ctx->d_gv.p, V, H, W, ctx->Wq, ctx->sc.Wp, ctx->stream) != 0)
+            throw Fail{MVS_E_HIP, "build_gv launch failed"};
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        ctx->sc.gv = ctx->d_gv.p;
+        for (int w = 0; w <= MVS_MAX_WID; ++w) ctx->sc.mom[w] = nullptr;
         mvs_tiled_geometry(W, H, &ctx->ntx, &ctx->nty);
         if (const char* vv = std::getenv("MVS_VARIANT")) ctx->variant = std::atoi(vv);
+        if (const char* cc = std::getenv("MVS_TILE_CHUNK")) ctx->chunk3 = std::max(32, std::min(512, std::atoi(cc)));
         if (const char* km = std::getenv("MVS_SCORE_KERNEL")) {
             if (!std::strcmp(km, "direct")) ctx->kernel_mode = 1;
             else if (!std::strcmp(km, "tiled")) ctx->kernel_mode = 2;

@@ -32,6 +32,15 @@ struct SceneDev {
     const uint8_t* stack;
     const uint8_t* rgb;      // V*H*W*3 (colour lookups of expansion candidates)
     const CamDev* cams;
+    // view-major gray copy gv[v][y][x] (row pitch Wp = W + 16): the reference
+    // view's window rows are read with scalar (SMEM) loads
+    const uint8_t* gv;
+    int Wp;
+    // per-view window moments mom[wid][(y*W + x)*V + v] = (S_b, S_bb) of the
+    // (2wid+1)^2 window centred at (x, y) (0 where the window is invalid);
+    // built once per scene and wid -- the np.mean/np.std ingredients of
+    // ctNcc, which do not depend on the reference view
+    const uint2* mom[MVS_MAX_WID + 1];
 };
 
 // Inputs/outputs of one scoring batch (device pointers).
@@ -98,6 +107,9 @@ extern "C" {
 int mvs_launch_build_stack(const uint8_t* d_rgb, uint8_t* d_stack, int V, int H, int W, int Wq,
                            hipStream_t s);
 int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s);
+int mvs_launch_build_gv(const uint8_t* d_stack, uint8_t* d_gv, int V, int H, int W, int Wq, int Wp,
+                        hipStream_t s);
+int mvs_launch_build_moments(const SceneDev* sc, int wid, uint2* d_mom, hipStream_t s);
 // Tile geometry of the tiled scorer for a W x H image (so the host can size scratch).
 void mvs_tiled_geometry(int W, int H, int* ntx, int* nty);
 int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,

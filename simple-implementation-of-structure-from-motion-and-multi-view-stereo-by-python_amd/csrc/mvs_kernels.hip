@@ -103,6 +103,32 @@ __device__ __forceinline__ double exact_ncc_stack(const SceneDev sc, int R, int 
     return exact_ncc_generic(A, B, NB * NB);
 }
 
+// Wave-wide binary64 sum without LDS: DPP butterflies inside each row of 16
+// lanes, then the four row sums combined from SGPRs.  Result in every lane.
+template <int CTRL>
+DEV double dpp_f64(double x) {
+    const unsigned long long u = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+DEV double wave_sum_dpp(double x) {
+    x += dpp_f64<0xB1>(x);    // quad_perm [1,0,3,2]
+    x += dpp_f64<0x4E>(x);    // quad_perm [2,3,0,1]
+    x += dpp_f64<0x141>(x);   // row_half_mirror
+    x += dpp_f64<0x140>(x);   // row_mirror: every lane holds its row's sum
+    const unsigned long long u = __double_as_longlong(x);
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, 16 * k);
+        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 16 * k);
+        r[k] = __longlong_as_double(((unsigned long long)hi << 32) | lo);
+    }
+    return (r[0] + r[1]) + (r[2] + r[3]);
+}
+
 DEV double wave_sum(double x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
@@ -156,13 +182,15 @@ DEV void wave_row(Fetch&& fetch, int row, int o, int V, int Rs, int Rl, int lane
 // counted from the quad holding column q - WID; o = (q - WID) & 3.
 // Lane 0 of the wave writes mask/count/avg.
 // Variants (A/B-able at run time, see mvs_launch_score_tiled):
+//   EPI 2: decision from exact-integer-fed squared comparison (no sqrt/div),
+//          relative band 1e-8 -> numpy order; value (for avg) by rsq+Newton
 //   EPI 0: decision from the binary64 closed form (guard 1e-9 -> numpy order)
 //   EPI 1: decision from a binary32 closed form (|err| < 4e-7; guard 1e-5 ->
 //          binary64 -> guard 1e-9 -> numpy order); binary64 only for lanes in
 //          the guard and, when avg is wanted, for passing lanes
 //   REF 0: reference-view words broadcast with v_readlane
 //   REF 1: reference-view words re-read by every lane (same LDS address = broadcast)
-template <int WID, int NS, bool UNROLL = false, int EPI = 0, int REF = 0, class Fetch,
+template <int WID, int NS, bool UNROLL = false, int EPI = 2, int REF = 0, class Fetch,
           class FetchRef>
 DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fetch&& fetch,
                          FetchRef&& fref, uint64_t* mask_out, int32_t* count_out,
@@ -285,7 +313,45 @@ DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fe
         auto ncc64 = [&]() {
             return (double)((int64_t)NPX * num) / ((double)(NPX - 1) * sqrt((double)da * (double)db));
         };
-        if constexpr (EPI == 0) {
+        if constexpr (EPI == 2) {
+            // Decision without sqrt/div: for thr >= 0.01, ncc > thr  <=>  L > 0 and
+            // L^2 > thr^2 (n-1)^2 da db  with L = n*num (exact in binary64).  The
+            // products carry < 1e-15 relative error; a relative band of 1e-8
+            // (|ncc - thr| < ~thr*5e-9) goes to the numpy-order path, far wider
+            // than the reference's own rounding (< 1e-12).
+            if (live) {
+                if (thr >= 0.01) {
+                    const double L = (double)((int64_t)NPX * num);
+                    if (L > 0.0) {
+                        const double tk = thr * (double)(NPX - 1);
+                        const double rhs = (tk * tk) * ((double)da * (double)db);
+                        const double diff = L * L - rhs;
+                        if (fabs(diff) <= 1e-8 * rhs) {
+                            ncc = exact_ncc_stack<WID>(sc, R, v, q, r);
+                            atomicAdd(exact_hits, 1);
+                            pass = ncc > thr;
+                        } else {
+                            pass = diff > 0.0;
+                            if (pass && avg_out) {
+                                // avg_ncc_score value only: rsq + two Newton steps
+                                const double D = (double)da * (double)db;
+                                double y = __builtin_amdgcn_rsq(D);
+                                y = y * (1.5 - 0.5 * D * y * y);
+                                y = y * (1.5 - 0.5 * D * y * y);
+                                ncc = L * y * (1.0 / (double)(NPX - 1));
+                            }
+                        }
+                    }
+                } else {
+                    ncc = ncc64();
+                    if (fabs(ncc - thr) <= kGuard) {
+                        ncc = exact_ncc_stack<WID>(sc, R, v, q, r);
+                        atomicAdd(exact_hits, 1);
+                    }
+                    pass = ncc > thr;
+                }
+            }
+        } else if constexpr (EPI == 0) {
             if (live) {
                 ncc = ncc64();
                 if (fabs(ncc - thr) <= kGuard) {
@@ -317,8 +383,11 @@ DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fe
         cnt += __popcll(m);
         acc += pass ? ncc : 0.0;
     }
-    if (EPI == 1 && !avg_out) {
-        if (lane == 0) *count_out = cnt;
+    if ((EPI != 0 && !avg_out) || cnt == 0) {
+        if (lane == 0) {
+            *count_out = cnt;
+            if (avg_out) *avg_out = 0.0;
+        }
         return;
     }
     const double tot = wave_sum(acc);
@@ -546,14 +615,41 @@ __global__ __launch_bounds__(256) void k_score_tiled(const SceneDev sc, const Sc
         const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
         const int y0 = ty * kTH - WID;                 // first region row
         const int kq0 = tx * (kTW / 4) + G::KQ0;       // first region quad
-        // stage: wave w copies (row, quad) pairs w, w+4, ...; lane = view
-        for (int pq = wave; pq < G::ROWS * G::NQ; pq += 4) {
-            const int ry = pq / G::NQ, kq = pq - ry * G::NQ;
-            const int y = y0 + ry, gq = kq0 + kq;
-            uint32_t val = 0;
-            if (lane < V && y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
-                val = *(const uint32_t*)(sc.stack + (int64_t)y * sc.row_bytes + (int64_t)gq * V * 4 + lane * 4);
-            lds[pq * QS + lane] = val;
+        // stage the region: 16-B chunks (4 views of one (row, quad)); each thread
+        // issues all its loads before its LDS writes so the fetches overlap
+        if ((V & 3) == 0) {
+            const int cpq = V >> 2, cpr = G::NQ * cpq, total = G::ROWS * cpr;
+            for (int base = 0; base < total; base += 8 * 256) {
+                uint4 buf[8];
+                int dst[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = base + u * 256 + (int)threadIdx.x;
+                    dst[u] = -1;
+                    buf[u] = make_uint4(0, 0, 0, 0);
+                    if (k < total) {
+                        const int ry = k / cpr, rem = k - ry * cpr;
+                        const int kq = rem / cpq, vq = rem - kq * cpq;
+                        const int y = y0 + ry, gq = kq0 + kq;
+                        if (y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                            buf[u] = *(const uint4*)(sc.stack + (int64_t)y * sc.row_bytes +
+                                                      (int64_t)gq * V * 4 + vq * 16);
+                        dst[u] = (ry * G::NQ + kq) * QS + vq * 4;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (dst[u] >= 0) *(uint4*)(lds + dst[u]) = buf[u];
+            }
+        } else {
+            for (int pq = wave; pq < G::ROWS * G::NQ; pq += 4) {
+                const int ry = pq / G::NQ, kq = pq - ry * G::NQ;
+                const int y = y0 + ry, gq = kq0 + kq;
+                uint32_t val = 0;
+                if (lane < V && y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                    val = *(const uint32_t*)(sc.stack + (int64_t)y * sc.row_bytes + (int64_t)gq * V * 4 + lane * 4);
+                lds[pq * QS + lane] = val;
+            }
         }
         __syncthreads();
         int2 nxt = cb + wave < ce ? t.sorted[cb + wave] : make_int2(0, 0);
@@ -574,6 +670,351 @@ __global__ __launch_bounds__(256) void k_score_tiled(const SceneDev sc, const Sc
                                                     a.exact_hits);
         }
         __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Scene-level precompute: view-major gray copy and per-view window moments
+// ---------------------------------------------------------------------------
+__global__ void k_build_gv(const uint8_t* __restrict__ stack, uint8_t* __restrict__ gv, int V, int H,
+                           int W, int Wq, int Wp) {
+    const int64_t total = (int64_t)V * H * Wp;
+    for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int x = (int)(id % Wp);
+        const int64_t vy = id / Wp;
+        const int y = (int)(vy % H), v = (int)(vy / H);
+        uint8_t g = 0;
+        if (x < W) g = stack[(int64_t)y * Wq * V * 4 + (int64_t)(x >> 2) * V * 4 + v * 4 + (x & 3)];
+        gv[id] = g;
+    }
+}
+
+// (S_b, S_bb) of every view's window at every valid centre; one thread per
+// (pixel, view), rows summed from the aligned words of the stack.
+template <int WID>
+__global__ void k_moments(const SceneDev sc, uint2* __restrict__ mom) {
+    constexpr int NB = 2 * WID + 1, NW = (NB + 3) / 4;
+    constexpr uint32_t LASTMASK = (NB % 4 == 0) ? 0xffffffffu : ((1u << (8 * (NB % 4))) - 1u);
+    const int64_t total = (int64_t)sc.H * sc.W * sc.V;
+    for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int v = (int)(id % sc.V);
+        const int64_t p = id / sc.V;
+        const int x = (int)(p % sc.W), y = (int)(p / sc.W);
+        uint2 out = make_uint2(0, 0);
+        if (y - WID >= 0 && y + WID + 1 < sc.H && x - WID > 0 && x + WID + 1 < sc.W) {
+            const int q0 = x - WID, k0 = q0 >> 2, o = q0 & 3;
+            uint32_t sb = 0, sbb = 0;
+            for (int row = 0; row < NB; ++row) {
+                const uint8_t* pr = sc.stack + (int64_t)(y - WID + row) * sc.row_bytes +
+                                    (int64_t)k0 * sc.V * 4 + v * 4;
+                uint32_t d[NW + 1];
+#pragma unroll
+                for (int j = 0; j <= NW; ++j) d[j] = *(const uint32_t*)(pr + (int64_t)j * sc.V * 4);
+#pragma unroll
+                for (int j = 0; j < NW; ++j) {
+                    uint32_t w = __builtin_amdgcn_alignbyte(d[j + 1], d[j], o);
+                    if (j == NW - 1) w &= LASTMASK;
+                    sb = __builtin_amdgcn_sad_u8(w, 0u, sb);
+                    sbb = __builtin_amdgcn_udot4(w, w, sbb, false);
+                }
+            }
+            out = make_uint2(sb, sbb);
+        }
+        mom[id] = out;
+    }
+}
+
+// Tiled scorer, v3: S_b/S_bb from the scene moments; S_ab from the
+// unaligned window quads in LDS against the reference view's quads loaded
+// by SMEM from the view-major copy and masked to the window (SALU) -- the
+// only per-row VALU work is NQW v_dot4_u32_u8.
+using cgu32 = __attribute__((address_space(4))) const uint32_t;
+
+// S_ab over the (2WID+1)^2 window whose first column sits at byte O of the
+// first quad: raw quads of this lane's view (own) against the reference
+// view's quads (ref, LDS broadcast) masked to the window at compile time --
+// interior quads need no mask, quads outside the window are skipped.
+template <int WID, int O>
+struct QuadMasks {
+    static constexpr int NB = 2 * WID + 1;
+    static constexpr int NQ = (O + NB + 3) / 4;
+    static constexpr uint32_t mask(int jj) {
+        const int st0 = O - 4 * jj, en0 = O + NB - 4 * jj;
+        const int st = st0 < 0 ? 0 : (st0 > 4 ? 4 : st0);
+        const int en = en0 < 0 ? 0 : (en0 > 4 ? 4 : en0);
+        const uint32_t hiM = en >= 4 ? 0xffffffffu : ((1u << (8 * en)) - 1u);
+        const uint32_t loM = (1u << (8 * st)) - 1u;
+        return en > st ? (hiM & ~loM) : 0u;
+    }
+};
+
+template <int WID, int O, int RS, int QS>
+DEV uint32_t sab_rows(const uint32_t* own, const uint32_t* ref) {
+    using M = QuadMasks<WID, O>;
+    constexpr int NB = 2 * WID + 1;
+    uint32_t d[NB][M::NQ], e[NB][M::NQ];
+#pragma unroll
+    for (int row = 0; row < NB; ++row)
+#pragma unroll
+        for (int jj = 0; jj < M::NQ; ++jj) {
+            d[row][jj] = own[row * RS + jj * QS];
+            e[row][jj] = ref[row * RS + jj * QS];
+        }
+    uint32_t ab[M::NQ];
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) ab[jj] = 0;
+#pragma unroll
+    for (int row = 0; row < NB; ++row)
+#pragma unroll
+        for (int jj = 0; jj < M::NQ; ++jj) {
+            constexpr uint32_t dummy = 0;
+            (void)dummy;
+            const uint32_t m = M::mask(jj);
+            const uint32_t am = (m == 0xffffffffu) ? e[row][jj] : (e[row][jj] & m);
+            ab[jj] = __builtin_amdgcn_udot4(am, d[row][jj], ab[jj], false);
+        }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) sum += ab[jj];
+    return sum;
+}
+
+// Same with the reference view's window quads loaded by SMEM (uniform
+// address, s_load) from the view-major copy: no LDS traffic and no VGPRs for
+// the reference side; masks applied on the SALU.
+template <int WID, int O, int RS, int QS>
+DEV uint32_t sab_rows_smem(const uint32_t* own, cgu32* ref, int ref_pitch_dw) {
+    using M = QuadMasks<WID, O>;
+    constexpr int NB = 2 * WID + 1;
+    uint32_t d[NB][M::NQ];
+#pragma unroll
+    for (int row = 0; row < NB; ++row)
+#pragma unroll
+        for (int jj = 0; jj < M::NQ; ++jj) d[row][jj] = own[row * RS + jj * QS];
+    uint32_t ab[M::NQ];
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) ab[jj] = 0;
+#pragma unroll
+    for (int row = 0; row < NB; ++row)
+#pragma unroll
+        for (int jj = 0; jj < M::NQ; ++jj) {
+            const uint32_t m = M::mask(jj);
+            const uint32_t e = ref[row * ref_pitch_dw + jj];
+            const uint32_t am = (m == 0xffffffffu) ? e : (e & m);
+            ab[jj] = __builtin_amdgcn_udot4(am, d[row][jj], ab[jj], false);
+        }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) sum += ab[jj];
+    return sum;
+}
+
+constexpr int kT3Threads = 256, kT3Waves = kT3Threads / 64;
+
+// Diagnostic build only (-DMVS_STAMPS): per-workgroup phase times of the
+// tiled kernel -- stage, candidates, write-out -- into a side buffer that no
+// output depends on.
+#ifdef MVS_STAMPS
+__device__ unsigned long long g_stamps[4096 * 8];
+#define STAMP(k)                                                                          \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        const unsigned long long ts_ = __builtin_amdgcn_s_memtime();                      \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) {                                      \
+            if ((k) == 0) st_prev = ts_;                                                  \
+            else { g_stamps[blockIdx.x * 8 + (k)] += ts_ - st_prev; st_prev = ts_; }      \
+            if ((k) == 3) g_stamps[blockIdx.x * 8] += 1;                                  \
+        }                                                                                 \
+    } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
+template <int WID, int QS, int REFSRC>
+__global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev sc, const ScoreArgs a,
+                                                                const TiledArgs t) {
+    using G = TileGeom<WID>;
+    constexpr int NB = 2 * WID + 1;
+    constexpr int NPX = NB * NB;
+    constexpr int NQW = (NB + 6) / 4;         // raw quads spanned by a row at any alignment
+    // QS: dwords per (row, quad) slot of the LDS image (= V when V == 48)
+    constexpr int RS = G::NQ * QS;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int V = sc.V;
+    const int n_items = t.item_off[t.ntiles];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint2* __restrict__ mom = sc.mom[WID];
+    // output staging behind the region image (chunk <= kChunk candidates)
+    uint64_t* o_mask = (uint64_t*)(lds + G::ROWS * RS);
+    double* o_avg = (double*)(o_mask + t.chunk);
+    int32_t* o_cnt = (int32_t*)(o_avg + t.chunk);
+    int32_t* o_idx = o_cnt + t.chunk;
+    __shared__ int s_item;
+#ifdef MVS_STAMPS
+    unsigned long long st_prev = 0;
+#endif
+    for (;;) {
+        // dynamic work queue: the next (tile, chunk) item for this workgroup
+        if (threadIdx.x == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
+        __syncthreads();
+        const int item = s_item;
+        if (item >= n_items) break;
+        STAMP(0);
+        int lo = 0, hi = t.ntiles;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t.item_off[mid] <= item) lo = mid; else hi = mid;
+        }
+        const int tile = lo;
+        const int chunk = item - t.item_off[tile];
+        const int cb = t.tile_off[tile] + chunk * t.chunk;
+        const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int y0 = ty * kTH - WID;
+        const int kq0 = tx * (kTW / 4) + G::KQ0;
+        {
+            const int cpq = V >> 2, cpr = G::NQ * cpq, total = G::ROWS * cpr;
+            for (int base = 0; base < total; base += 8 * kT3Threads) {
+                uint4 buf[8];
+                int dst[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = base + u * kT3Threads + (int)threadIdx.x;
+                    dst[u] = -1;
+                    buf[u] = make_uint4(0, 0, 0, 0);
+                    if (k < total) {
+                        const int ry = k / cpr, rem = k - ry * cpr;
+                        const int kq = rem / cpq, vq = rem - kq * cpq;
+                        const int y = y0 + ry, gq = kq0 + kq;
+                        if (y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                            buf[u] = *(const uint4*)(sc.stack + (int64_t)y * sc.row_bytes +
+                                                      (int64_t)gq * V * 4 + vq * 16);
+                        dst[u] = (ry * G::NQ + kq) * QS + vq * 4;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (dst[u] >= 0) *(uint4*)(lds + dst[u]) = buf[u];
+            }
+        }
+        __syncthreads();
+        STAMP(1);
+        // Candidates: outputs go to an LDS staging slot and leave the CU after
+        // the loop, so no wave ever waits on its own stores (vmcnt counts
+        // stores and loads together, in order).  The next candidate's entry
+        // (SMEM) and moments (VMEM) are fetched one iteration ahead.
+        auto sload = [](const int2* p) -> int2 {   // uniform address -> s_load_dwordx2
+            const unsigned long long v = *(const __attribute__((address_space(4))) unsigned long long*)p;
+            return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+        };
+        int2 cur = cb + wave < ce ? sload(t.sorted + cb + wave) : make_int2(0, 0);
+        uint2 mb_cur = make_uint2(0, 0);
+        if (cb + wave < ce) {
+            const int pk = cur.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
+            if (lane < V) mb_cur = mom[(r * sc.W + q) * V + lane];
+        }
+        for (int j = cb + wave; j < ce; j += kT3Waves) {
+            const int2 nxt = j + kT3Waves < ce ? sload(t.sorted + j + kT3Waves) : make_int2(0, 0);
+            uint2 mb_nxt = make_uint2(0, 0);
+            if (j + kT3Waves < ce) {
+                const int pk = nxt.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
+                if (lane < V) mb_nxt = mom[(r * sc.W + q) * V + lane];
+            }
+            const int pk = cur.y;
+            const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
+            const int q0 = q - WID, o = q0 & 3;
+            const int k0 = (q0 >> 2) - kq0;
+            const uint2 mb = mb_cur;
+            const uint2 ma = make_uint2(__builtin_amdgcn_readlane(mb.x, R), __builtin_amdgcn_readlane(mb.y, R));
+            const uint32_t* basep = lds + (r - WID - y0) * RS + k0 * QS + lane;
+            // the reference view's quads: same LDS address in every lane (broadcast)
+            const uint32_t* refl = basep - lane + R;
+            uint32_t Sab;
+            if constexpr (REFSRC == 0) {
+                switch (o) {   // wave-uniform: window byte offset inside the first quad
+                    case 0: Sab = sab_rows<WID, 0, RS, QS>(basep, refl); break;
+                    case 1: Sab = sab_rows<WID, 1, RS, QS>(basep, refl); break;
+                    case 2: Sab = sab_rows<WID, 2, RS, QS>(basep, refl); break;
+                    default: Sab = sab_rows<WID, 3, RS, QS>(basep, refl); break;
+                }
+            } else {
+                cgu32* refg = (cgu32*)(sc.gv + ((int64_t)R * sc.H + (r - WID)) * sc.Wp + 4 * (q0 >> 2));
+                const int pitch = sc.Wp >> 2;
+                switch (o) {
+                    case 0: Sab = sab_rows_smem<WID, 0, RS, QS>(basep, refg, pitch); break;
+                    case 1: Sab = sab_rows_smem<WID, 1, RS, QS>(basep, refg, pitch); break;
+                    case 2: Sab = sab_rows_smem<WID, 2, RS, QS>(basep, refg, pitch); break;
+                    default: Sab = sab_rows_smem<WID, 3, RS, QS>(basep, refg, pitch); break;
+                }
+            }
+            // |num|, da, db < 2^31 for windows up to 11x11 (sums < 2^24): 24-bit
+            // multiplies, exact
+            static_assert(NPX <= 121, "24-bit moment products need NB <= 11");
+            const int32_t da = (int32_t)(__umul24(NPX, ma.y) - __umul24(ma.x, ma.x));
+            const int32_t db = (int32_t)(__umul24(NPX, mb.y) - __umul24(mb.x, mb.x));
+            const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma.x, mb.x));
+            const bool live = lane < V && lane != R && da > 0 && db > 0;
+            bool pass = false;
+            double ncc = 0.0;
+            if (live) {
+                if (a.thr >= 0.01) {
+                    const double L = (double)num * (double)NPX;
+                    if (L > 0.0) {
+                        const double tk = a.thr * (double)(NPX - 1);
+                        const double rhs = (tk * tk) * ((double)da * (double)db);
+                        const double diff = L * L - rhs;
+                        if (fabs(diff) <= 1e-8 * rhs) {
+                            ncc = exact_ncc_stack<WID>(sc, R, lane, q, r);
+                            atomicAdd(a.exact_hits, 1);
+                            pass = ncc > a.thr;
+                        } else {
+                            pass = diff > 0.0;
+                            if (pass && a.avg) {
+                                const double D = (double)da * (double)db;
+                                double y = __builtin_amdgcn_rsq(D);
+                                y = y * (1.5 - 0.5 * D * y * y);
+                                y = y * (1.5 - 0.5 * D * y * y);
+                                ncc = L * y * (1.0 / (double)(NPX - 1));
+                            }
+                        }
+                    }
+                } else {
+                    ncc = ((double)num * (double)NPX) /
+                          ((double)(NPX - 1) * sqrt((double)da * (double)db));
+                    if (fabs(ncc - a.thr) <= kGuard) {
+                        ncc = exact_ncc_stack<WID>(sc, R, lane, q, r);
+                        atomicAdd(a.exact_hits, 1);
+                    }
+                    pass = ncc > a.thr;
+                }
+            }
+            const uint64_t m = __ballot(pass);
+            const int cnt = __popcll(m);
+            double avgv = 0.0;
+            if (a.avg && cnt) avgv = wave_sum_dpp(pass ? ncc : 0.0) / cnt;
+            const int slot = j - cb;
+            if (lane == 0) {
+                o_mask[slot] = m;
+                o_avg[slot] = avgv;
+                o_cnt[slot] = cnt;
+                o_idx[slot] = cur.x;
+            }
+            cur = nxt;
+            mb_cur = mb_nxt;
+        }
+        __syncthreads();
+        STAMP(2);
+        for (int k = threadIdx.x; k < ce - cb; k += blockDim.x) {
+            const int i = o_idx[k];
+            a.mask[i] = o_mask[k];
+            a.count[i] = o_cnt[k];
+            if (a.avg) a.avg[i] = o_avg[k];
+        }
+        __syncthreads();
+        STAMP(3);
     }
 }
 
@@ -730,11 +1171,26 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
     const size_t lds = (size_t)G::ROWS * G::NQ * 64 * 4;
+    if (variant == 4 || variant == 5 || (variant == 0 && sc->mom[WID] != nullptr)) {
+        if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kChunk) return -3;
+        const size_t outs = (size_t)t->chunk * (8 + 8 + 4 + 4);
+        const bool smem = variant == 4;
+        if (sc->V == 48 && variant != 5) {
+            const size_t lds3 = (size_t)G::ROWS * G::NQ * 48 * 4 + outs;
+            if (smem) hipLaunchKernelGGL((k_score_tiled3<WID, 48, 1>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
+            else hipLaunchKernelGGL((k_score_tiled3<WID, 48, 0>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
+        } else {
+            const size_t lds3 = (size_t)G::ROWS * G::NQ * 64 * 4 + outs;
+            if (smem) hipLaunchKernelGGL((k_score_tiled3<WID, 64, 1>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
+            else hipLaunchKernelGGL((k_score_tiled3<WID, 64, 0>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     switch (variant) {
-        case 0: hipLaunchKernelGGL((k_score_tiled<WID, 0, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
-        case 1: hipLaunchKernelGGL((k_score_tiled<WID, 1, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
-        case 2: hipLaunchKernelGGL((k_score_tiled<WID, 0, 1>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
-        default: hipLaunchKernelGGL((k_score_tiled<WID, 1, 1>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+        case 0: hipLaunchKernelGGL((k_score_tiled<WID, 2, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+        case 1: hipLaunchKernelGGL((k_score_tiled<WID, 2, 1>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+        case 2: hipLaunchKernelGGL((k_score_tiled<WID, 0, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
+        default: hipLaunchKernelGGL((k_score_tiled<WID, 1, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -759,6 +1215,34 @@ extern "C" int mvs_launch_build_stack(const uint8_t* d_rgb, uint8_t* d_stack, in
     const int64_t total = (int64_t)H * Wq * V;
     const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
     hipLaunchKernelGGL(k_build_stack, dim3(blocks), dim3(256), 0, s, d_rgb, d_stack, V, H, W, Wq);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mvs_read_stamps(unsigned long long* out) {
+#ifdef MVS_STAMPS
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4096 * 8) != hipSuccess) return -1;
+    return 0;
+#else
+    (void)out;
+    return -3;
+#endif
+}
+
+extern "C" int mvs_launch_build_gv(const uint8_t* d_stack, uint8_t* d_gv, int V, int H, int W, int Wq,
+                                   int Wp, hipStream_t s) {
+    hipLaunchKernelGGL(k_build_gv, dim3(4096), dim3(256), 0, s, d_stack, d_gv, V, H, W, Wq, Wp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mvs_launch_build_moments(const SceneDev* sc, int wid, uint2* d_mom, hipStream_t s) {
+    switch (wid) {
+        case 1: hipLaunchKernelGGL(k_moments<1>, dim3(8192), dim3(256), 0, s, *sc, d_mom); break;
+        case 2: hipLaunchKernelGGL(k_moments<2>, dim3(8192), dim3(256), 0, s, *sc, d_mom); break;
+        case 3: hipLaunchKernelGGL(k_moments<3>, dim3(8192), dim3(256), 0, s, *sc, d_mom); break;
+        case 4: hipLaunchKernelGGL(k_moments<4>, dim3(8192), dim3(256), 0, s, *sc, d_mom); break;
+        case 5: hipLaunchKernelGGL(k_moments<5>, dim3(8192), dim3(256), 0, s, *sc, d_mom); break;
+        default: return -2;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -113,6 +113,33 @@ def test_score_dense_tile(kctx, oracle_scene, dino):
         assert np.array_equal(g, e)
 
 
+def test_score_threshold_on_reference_value(kctx, oracle_scene, dino):
+    """Thresholds placed exactly on (and one ulp around) the reference's
+    ctNcc value of a view: the kernel's guard band must route the decision
+    through the numpy-order path and agree with the strict `ncc > thr`."""
+    rgb, K, R, t = dino
+    c, ref = bench_candidates(400, K, R, t, seed=21)
+    hits0 = kctx.exact_hits()
+    checked = 0
+    for i in range(len(ref)):
+        ncc = oracle_scene.photo_ncc(c[i], ref[i], 5)
+        fin = np.nonzero(np.isfinite(ncc) & (ncc > 0.05))[0]
+        if len(fin) == 0:
+            continue
+        v = fin[len(fin) // 2]
+        for thr in (ncc[v], np.nextafter(ncc[v], 2.0), np.nextafter(ncc[v], -2.0)):
+            cc, rr = np.tile(c[i], (3000, 1)), np.full(3000, ref[i], np.int32)   # >= 2048: tiles too
+            got = kctx.score(cc, rr, float(thr), 5)
+            exp = oracle_scene.score_batch(cc[:1], rr[:1], float(thr), 5)
+            assert np.array_equal(got[1][:1], exp[1]), (i, v, thr)
+            assert (got[1] == got[1][0]).all()
+        checked += 1
+        if checked >= 12:
+            break
+    assert checked >= 5
+    assert kctx.exact_hits() > hits0
+
+
 def test_score_empty_batch(ctx):
     xy, mask, count, avg = ctx.score(np.zeros((0, 3)), np.zeros(0, np.int32))
     assert len(count) == 0
