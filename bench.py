@@ -70,12 +70,13 @@ def main():
         os.environ["MVS_SCORE_KERNEL"] = a.kernel
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     pkg = importlib.import_module(PKG_NAME)
+    par = importlib.import_module(PKG_NAME + ".parallel")
 
     rgb, K, R, t = load_scene()
     V = len(rgb)
@@ -102,23 +103,10 @@ def main():
         if evs is not None:
             evs[1].record(stream)
         if world > 1:
-            # the sweep's exchange: accepted records (index, count, mask, xy) to every rank
-            acc = torch.nonzero(count >= vlb).squeeze(1)
-            k = torch.tensor([acc.numel()], device=dev, dtype=torch.int64)
-            ks = [torch.empty_like(k) for _ in range(world)]
-            dist.all_gather(ks, k)
-            kmax = max(int(x.item()) for x in ks)
-            recw = 2 + words + 2
-            buf = torch.zeros((max(kmax, 1), recw), dtype=torch.int64, device=dev)
-            m = acc.numel()
-            if m:
-                buf[:m, 0] = acc
-                buf[:m, 1] = count[acc].to(torch.int64)
-                buf[:m, 2:2 + words] = mask[acc]
-                buf[:m, 2 + words:] = xy[acc].view(torch.int64)
-            out = torch.empty((world * buf.shape[0], recw), dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(out, buf)
-            gathered["n"] = sum(int(x.item()) for x in ks)
+            # the sweep's exchange (parallel.py): accepted records to every rank
+            rec = par.pack_accepted(rank * n, count, mask, xy, vlb)
+            allrec = par.all_gather_records(rec)
+            gathered["n"] = int(allrec.shape[0])
 
     def timed(wid, steps, warmup):
         for _ in range(warmup):

@@ -1,0 +1,53 @@
+"""Entry point with the reference's flags (main.py:33-42 of the reference):
+
+    python main.py -img_p data/dinoRing -par_p data/dinoRing/dinoR_par.txt -t png -scale 10 \
+                   -seeds tests/golden/seeds_dino.npz
+
+The MVS stage (DensePointsWithMVS2, MVS2.py:176) runs on the GPU through
+libmvs_amd.so and writes initial_patches.ply / all_patches.ply in the working
+directory, like the reference.  The reference's SfM stage (ORB + FLANN +
+RANSAC through OpenCV, SFM.py) is not part of this build: its output -- the
+GlobalSet tracks -- is read from -seeds (npz with track_off, obs_view, obs_xy,
+the format tests/golden/make_seeds.py writes).
+"""
+import importlib
+import os
+import sys
+from argparse import ArgumentParser
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_NAME = "simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd"
+sys.path.insert(0, REPO)
+
+
+def main(args):
+    mvs = importlib.import_module(PKG_NAME)
+    imgs = mvs.read_imgs(args)
+    if not args.seeds:
+        raise RuntimeError("no SfM tracks: this build has no OpenCV SfM stage; pass -seeds FILE.npz")
+    global_set = mvs.SeedSet.load(args.seeds)
+    mvs.DensePointsWithMVS2(imgs, global_set, args, max_pops=args.max_pops)
+    st = mvs.MVS2.last_stats
+    print("pops {pops} tests {tests} accepted {accepts} gpu-scored {scored} sweeps {sweeps}".format(**st))
+
+
+if __name__ == "__main__":
+    parser = ArgumentParser()
+    parser.add_argument("-img_p", help="image directory", dest="img_dir", default=None)
+    parser.add_argument("-par_p", help="parameter path", dest="par_path", default=None)
+    parser.add_argument("-t", help="image file type", dest="img_type", default="ppm")
+    parser.add_argument("-scale", help="scale", dest="scale", default=1, type=float)
+    parser.add_argument("--debug", help="debug mode on", dest="debug", action="store_true")
+    parser.add_argument("--nonSequence", help="", dest="nonSeq", action="store_true")
+    parser.add_argument("-cell_size", help="", dest="cell_size", default=2, type=int)
+    parser.add_argument("-desc_wid", help="", dest="desc_wid", default=5, type=int)
+    parser.add_argument("-seeds", help="SfM tracks (npz: track_off, obs_view, obs_xy)",
+                        dest="seeds", default=None)
+    parser.add_argument("-max_pops", help="expansion pop cap (<= 100000)", dest="max_pops",
+                        default=100000, type=int)
+    args = parser.parse_args()
+    try:
+        main(args)
+    except RuntimeError as e:
+        print("RuntimeError", e)
+        sys.exit(1)

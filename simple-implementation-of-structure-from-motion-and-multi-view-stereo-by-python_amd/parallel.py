@@ -1,0 +1,80 @@
+"""Multi-GPU sweeps: candidate batches sharded over ranks, accepted records
+all-gathered (RCCL over xGMI on MI355X, gloo on CPU for tests).
+
+One process per GPU (torch.distributed, backend "nccl" == RCCL on ROCm).
+Every candidate's photo test depends only on read-only data (images,
+cameras), so a sweep's candidates split into contiguous per-rank slices with
+no communication while scoring.  The only exchange is at the end of the
+sweep: each rank packs the candidates it accepted (|V| >= vlb,
+MVS2.py:256/369) as fixed-width int64 records and all-gathers them, so every
+rank holds the sweep's accepted set -- the input of the replicated,
+order-deterministic commit.
+
+Record layout (int64 columns): [global index, count, mask words..., x bits, y bits].
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n, rank, world):
+    """Contiguous slice [begin, end) of n items for `rank` (sizes differ by <= 1)."""
+    base, extra = divmod(n, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def record_width(words):
+    return 2 + words + 2
+
+
+def pack_accepted(offset, count, mask, xy, vlb):
+    """Accepted candidates of this rank's slice as int64 records (k, record_width)."""
+    acc = torch.nonzero(count >= vlb).squeeze(1)
+    words = mask.shape[1]
+    rec = torch.empty((acc.numel(), record_width(words)), dtype=torch.int64, device=count.device)
+    if acc.numel():
+        rec[:, 0] = acc + offset
+        rec[:, 1] = count[acc].to(torch.int64)
+        rec[:, 2:2 + words] = mask[acc].view(torch.int64)
+        rec[:, 2 + words:] = xy[acc].contiguous().view(torch.int64)
+    return rec
+
+
+def all_gather_records(rec, group=None):
+    """All-gather variable-length record blocks; returns them concatenated in rank order."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return rec
+    k = torch.tensor([rec.shape[0]], dtype=torch.int64, device=rec.device)
+    ks = [torch.empty_like(k) for _ in range(world)]
+    dist.all_gather(ks, k, group=group)
+    sizes = [int(x.item()) for x in ks]
+    kmax = max(max(sizes), 1)
+    buf = torch.zeros((kmax, rec.shape[1]), dtype=rec.dtype, device=rec.device)
+    buf[:rec.shape[0]] = rec
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf, group=group)
+    return torch.cat([o[:s] for o, s in zip(outs, sizes)], 0)
+
+
+def unpack_records(rec, words):
+    """-> (index, count, mask (k, words) uint64 view as int64, xy (k, 2) float64)."""
+    idx = rec[:, 0]
+    count = rec[:, 1].to(torch.int32)
+    mask = rec[:, 2:2 + words]
+    xy = rec[:, 2 + words:].contiguous().view(torch.float64)
+    return idx, count, mask, xy
+
+
+def sharded_sweep(score_fn, c, ref, vlb, words, group=None):
+    """Score the sweep [c, ref] (all ranks pass the same full batch) by slices and
+    exchange the accepted records.  score_fn(c_slice, ref_slice) -> (xy, mask, count)
+    as tensors.  Returns (index, count, mask, xy) of every accepted candidate of the
+    sweep, in global index order, identical on every rank."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    b, e = shard_range(len(ref), rank, world)
+    xy, mask, count = score_fn(c[b:e], ref[b:e])
+    rec = pack_accepted(b, count, mask, xy, vlb)
+    allrec = all_gather_records(rec, group) if world > 1 else rec
+    return unpack_records(allrec, words)

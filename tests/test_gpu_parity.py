@@ -281,3 +281,51 @@ def test_view_count_variants(pkg, orc, V):
             for g, e in zip(got[:3], exp[:3]):
                 assert np.array_equal(g, e)
             np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+
+
+def test_stage_full_run_vs_oracle_fixture(ctx, seeds):
+    """The reference's own 100,000-pop cap (MVS2.py:321): every accepted patch,
+    in order, bit-exact against the oracle's full run (counts + sha256)."""
+    import hashlib
+    import json
+    import os
+    from conftest import GOLDEN
+    p = os.path.join(GOLDEN, "stage_oracle_cap100000.json")
+    if not os.path.exists(p):
+        pytest.skip("full-run oracle fixture not generated")
+    j = json.load(open(p))
+    ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
+                              cell_size=2, scale=10.0, wid=5, max_pops=100000)
+    assert st["pops"] == j["stats"]["pops"]
+    assert st["tests"] == j["stats"]["tests"]
+    assert st["queue_left"] == j["stats"]["queue_left"]
+    assert len(ini) == j["n_initial"] and len(allp) == j["n_all"]
+    assert hashlib.sha256(np.ascontiguousarray(ini, "<f8").tobytes()).hexdigest() == j["sha256_initial"]
+    assert hashlib.sha256(np.ascontiguousarray(allp, "<f8").tobytes()).hexdigest() == j["sha256_all"]
+
+
+def test_main_entry_point(pkg, tmp_path, monkeypatch):
+    """main.py with the reference's flags writes the two PLYs of the stage."""
+    import importlib.util
+    import os
+    from conftest import DATA, GOLDEN, REPO
+    spec = importlib.util.spec_from_file_location("mvs_main", os.path.join(REPO, "main.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    monkeypatch.chdir(tmp_path)
+
+    class A:
+        img_dir = DATA
+        par_path = os.path.join(DATA, "dinoR_par.txt")
+        img_type = "png"
+        scale = 10.0
+        debug = False
+        nonSeq = False
+        cell_size = 2
+        desc_wid = 5
+        seeds = os.path.join(GOLDEN, "seeds_dino.npz")
+        max_pops = 200
+    m.main(A())
+    g = stage_golden(200)
+    assert np.array_equal(pkg.read_ply(str(tmp_path / "initial_patches.ply")), g["initial_patches"])
+    assert np.array_equal(pkg.read_ply(str(tmp_path / "all_patches.ply")), g["all_patches"])
