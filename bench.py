@@ -26,6 +26,7 @@ PKG_NAME = "simple-implementation-of-structure-from-motion-and-multi-view-stereo
 sys.path.insert(0, REPO)
 
 PEAK_HBM = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
+KERNEL_NAME = {"auto": "k_score_tiled3", "tiled": "k_score_tiled3", "direct": "k_score"}
 
 
 def algorithmic_bytes(V, wid):
@@ -57,7 +58,8 @@ def main():
     ap.add_argument("--wid", type=int, default=5)
     ap.add_argument("--thr", type=float, default=0.7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=100000)
+    ap.add_argument("--cpu-sample", type=int, default=500000,
+                    help="candidates the single-threaded oracle scores (~10 s)")
     ap.add_argument("--secondary-wid", type=int, default=3)
     ap.add_argument("--kernel", choices=["auto", "direct", "tiled"], default="auto",
                     help="scoring kernel (MVS_SCORE_KERNEL)")
@@ -116,6 +118,7 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        ctx.kernel_timing(True)     # HIP events around the dominant kernel, on its stream
         t0 = time.perf_counter()
         for k in range(steps):
             step(wid, evs[k])
@@ -123,14 +126,19 @@ def main():
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        kms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / steps   # score kernel, HIP events
+        ctx.kernel_timing(False)
+        kt, kl = ctx.kernel_time()
+        if kl != steps or kt <= 0.0:
+            raise RuntimeError(f"kernel timing recorded {kl} launches / {kt} ms for {steps} steps")
+        kms = kt / kl                                                    # dominant kernel
+        pms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / steps   # whole scoring call
         if world > 1:
             tt = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
-        return dt, kms
+        return dt, kms, pms
 
-    dt, kms = timed(a.wid, a.steps, a.warmup)
+    dt, kms, pms = timed(a.wid, a.steps, a.warmup)
     total = n * world * a.steps
     value = total / dt
     B = algorithmic_bytes(V, a.wid)
@@ -138,7 +146,7 @@ def main():
     accepted = int((count >= vlb).sum().item())
     sec = None
     if a.secondary_wid and a.secondary_wid != a.wid:
-        dt2, kms2 = timed(a.secondary_wid, max(a.steps // 2, 5), 2)
+        dt2, kms2, _ = timed(a.secondary_wid, max(a.steps // 2, 5), 2)
         B2 = algorithmic_bytes(V, a.secondary_wid)
         sec = {"wid": a.secondary_wid, "value": n * world * max(a.steps // 2, 5) / dt2,
                "kernel_ms": kms2, "achieved_GBps": B2 * n / (kms2 * 1e-3) / 1e9}
@@ -196,8 +204,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM,
                          "traffic": traffic,
-                         "kernel": a.kernel,
-                         "kernel_ms": kms, "bytes_per_candidate": B},
+                         "kernel": KERNEL_NAME[a.kernel] if V <= 64 else "k_score",
+                         "kernel_ms": kms, "score_call_ms": pms,
+                         "bytes_per_candidate": B, "candidates_per_launch": n},
             "cpu_baseline": cpu,
             "accepted_per_sweep": accepted,
             "gathered_records": gathered["n"],

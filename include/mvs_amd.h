@@ -72,8 +72,18 @@ int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int 
 int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
                      double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
                      double* d_avg, void* stream);
-/* Number of per-view NCC decisions that fell within 1e-9 of the threshold
- * and were re-evaluated in numpy order since the context was created. */
+/* Kernel timing (measurement only): while enabled, every scoring call records a
+ * HIP event pair on its stream immediately around the dominant scoring kernel
+ * (k_score_tiled3, or k_score for small/large-V batches).  enable != 0 resets
+ * the record and turns it on; 0 turns it off (the record stays readable).
+ * mvs_kernel_time synchronises the recorded events and returns the summed
+ * kernel time and the number of timed launches. */
+int mvs_kernel_timing(mvs_ctx* ctx, int enable);
+int mvs_kernel_time(mvs_ctx* ctx, double* total_ms, int64_t* launches);
+/* Number of per-view NCC decisions that fell inside the guard band around the
+ * threshold (relative 1e-8 on the squared comparison; 1e-9 absolute when
+ * min_ncc < 0.01) and were re-evaluated in numpy order since the context was
+ * created. */
 int64_t mvs_exact_hits(mvs_ctx* ctx);
 
 /* ctNcc (MVS2.py:39-43) on n explicit window pairs of npx (<= 128) uint8

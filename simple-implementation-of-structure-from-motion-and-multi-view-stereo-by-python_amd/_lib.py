@@ -33,6 +33,9 @@ SIGNATURES = [
     ("mvs_score_device", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int,
                                         ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
     ("mvs_exact_hits", ctypes.c_int64, [_vp]),
+    ("mvs_kernel_timing", ctypes.c_int, [_vp, ctypes.c_int]),
+    ("mvs_kernel_time", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_int64)]),
     ("mvs_ncc_windows", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_double,
                                        ctypes.c_int, _vp, _vp, _vp]),
     ("mvs_stage_run", ctypes.c_int, [_vp, ctypes.c_int64, _i64p, _i32p, _fp, ctypes.c_int,
@@ -167,6 +170,18 @@ class MvsContext:
 
     def exact_hits(self):
         return int(load().mvs_exact_hits(self._h))
+
+    def kernel_timing(self, enable=True):
+        """Start (reset) or stop HIP-event timing of the dominant scoring kernel."""
+        check(load().mvs_kernel_timing(self._h, 1 if enable else 0), self._h, "mvs_kernel_timing")
+
+    def kernel_time(self):
+        """-> (total kernel milliseconds, timed launches) since kernel_timing(True)."""
+        ms = ctypes.c_double(0.0)
+        k = ctypes.c_int64(0)
+        check(load().mvs_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(k)), self._h,
+              "mvs_kernel_time")
+        return ms.value, int(k.value)
 
     def score(self, c, ref, min_ncc=0.7, wid=5):
         """Batched photo_consistenecy_test (MVS2.py:62-77) on host arrays.

@@ -281,12 +281,30 @@ struct mvs_ctx {
     DevBuf<int32_t> s_ref, s_count;
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
-    int ntx = 0, nty = 0;
     DevBuf<int32_t> t_tiles, t_cand;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
     int variant = 0;       // tiled-kernel variant (env MVS_VARIANT), see mvs_kernels.hip
     int chunk3 = 256;      // candidates per work item of the v3 tiled kernel (env MVS_TILE_CHUNK)
+    // kernel timing (mvs_kernel_timing): one event pair per scoring launch
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
     std::string err;
+    // next event pair while timing is on, else nulls
+    void next_events(hipEvent_t* e0, hipEvent_t* e1) {
+        *e0 = *e1 = nullptr;
+        if (!timing) return;
+        if (ev_used + 2 > ev.size()) {
+            for (int k = 0; k < 2; ++k) {
+                hipEvent_t e;
+                HIPCHK(hipEventCreate(&e));
+                ev.push_back(e);
+            }
+        }
+        *e0 = ev[ev_used];
+        *e1 = ev[ev_used + 1];
+        ev_used += 2;
+    }
     int words() const { return (V + 63) / 64; }
 };
 
@@ -359,7 +377,9 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
     a.avg = d_avg;
     a.exact_hits = ctx->d_exact.p;
     const bool tiled = ctx->V <= 64 && (ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048));
-    if (tiled && (ctx->variant == 4 || ctx->variant == 5 || ctx->variant == 0) && (ctx->V & 3) == 0 &&
+    // the MFMA scorer stages 16-B groups of 4 views: other view counts take the 16x8 tiled path
+    const int variant = (ctx->variant == 6 && (ctx->V & 3) != 0) ? 0 : ctx->variant;
+    if (tiled && (variant == 4 || variant == 5 || variant == 6 || variant == 0) && (ctx->V & 3) == 0 &&
         !ctx->sc.mom[wid]) {
         // scene moments for this window size: built once, reused by every batch
         ctx->d_mom[wid].alloc((size_t)ctx->H * ctx->W * ctx->V);
@@ -368,26 +388,32 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         ctx->sc.mom[wid] = ctx->d_mom[wid].p;
     }
     if (tiled) {
-        const int ntiles = ctx->ntx * ctx->nty;
-        ctx->t_tiles.ensure((size_t)3 * (ntiles + 1));
-        ctx->t_cand.ensure((size_t)5 * n);
+        const bool mfma = variant == 6;
         TiledArgs t{};
-        t.ntx = ctx->ntx;
-        t.nty = ctx->nty;
+        mvs_tiled_geometry(ctx->W, ctx->H, mfma ? 1 : 0, &t.tw, &t.th, &t.ntx, &t.nty);
+        const int ntiles = t.ntx * t.nty;
+        ctx->t_tiles.ensure((size_t)3 * (ntiles + 2));
+        ctx->t_cand.ensure((size_t)6 * n);
         t.ntiles = ntiles;
-        t.chunk = (ctx->variant == 0 || ctx->variant >= 4) ? ctx->chunk3 : 512;
+        t.chunk = mfma ? 1024 : (variant == 0 || variant >= 4) ? ctx->chunk3 : 512;
         t.tile_count = ctx->t_tiles.p;
-        t.tile_off = ctx->t_tiles.p + (ntiles + 1);
-        t.item_off = ctx->t_tiles.p + 2 * (ntiles + 1);
+        t.tile_off = ctx->t_tiles.p + (ntiles + 2);
+        t.item_off = ctx->t_tiles.p + 2 * (ntiles + 2);
+        t.fix_count = ctx->t_tiles.p + ntiles + 1;
         t.cand_key = ctx->t_cand.p;
         t.cand_rank = ctx->t_cand.p + n;
         t.cand_pk = ctx->t_cand.p + 2 * n;
         t.sorted = (int2*)(ctx->t_cand.p + 3 * n);
-        if (mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, ctx->variant, s) != 0)
+        t.fix_list = ctx->t_cand.p + 5 * n;
+        hipEvent_t e0, e1;
+        ctx->next_events(&e0, &e1);
+        if (mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, variant, s, e0, e1) != 0)
             throw Fail{MVS_E_HIP, "tiled score launch failed"};
         return;
     }
-    if (mvs_launch_score(&ctx->sc, &a, wid, s) != 0) throw Fail{MVS_E_HIP, "score launch failed"};
+    hipEvent_t e0, e1;
+    ctx->next_events(&e0, &e1);
+    if (mvs_launch_score(&ctx->sc, &a, wid, s, e0, e1) != 0) throw Fail{MVS_E_HIP, "score launch failed"};
 }
 
 // ---------------------------------------------------------------------------
@@ -826,7 +852,6 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
         HIPCHK(hipStreamSynchronize(ctx->stream));
         ctx->sc.gv = ctx->d_gv.p;
         for (int w = 0; w <= MVS_MAX_WID; ++w) ctx->sc.mom[w] = nullptr;
-        mvs_tiled_geometry(W, H, &ctx->ntx, &ctx->nty);
         if (const char* vv = std::getenv("MVS_VARIANT")) ctx->variant = std::atoi(vv);
         if (const char* cc = std::getenv("MVS_TILE_CHUNK")) ctx->chunk3 = std::max(32, std::min(512, std::atoi(cc)));
         if (const char* km = std::getenv("MVS_SCORE_KERNEL")) {
@@ -848,7 +873,33 @@ void mvs_ctx_destroy(mvs_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
     delete ctx;
+}
+
+int mvs_kernel_timing(mvs_ctx* ctx, int enable) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    return guarded(ctx, [&]() {
+        ctx->timing = enable != 0;
+        if (ctx->timing) ctx->ev_used = 0;   // disabling keeps the record readable
+        return 0;
+    });
+}
+
+int mvs_kernel_time(mvs_ctx* ctx, double* total_ms, int64_t* launches) {
+    if (!ctx || !total_ms || !launches) return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
+    return guarded(ctx, [&]() {
+        double tot = 0.0;
+        for (size_t k = 0; k + 1 < ctx->ev_used; k += 2) {
+            HIPCHK(hipEventSynchronize(ctx->ev[k + 1]));
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, ctx->ev[k], ctx->ev[k + 1]));
+            tot += ms;
+        }
+        *total_ms = tot;
+        *launches = (int64_t)(ctx->ev_used / 2);
+        return 0;
+    });
 }
 
 int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp) {

@@ -60,8 +60,11 @@ struct ScoreArgs {
 //   tile_count[ntiles+1], tile_off[ntiles+1], item_off[ntiles+1], n_items[1]
 //   cand_key[n]  = tile (or -1 if the window is invalid), cand_rank[n],
 //   cand_pk[n]   = q | r << 11 | R << 22, sorted[n] = {id, pk} grouped by tile
+//   fix_list[n], fix_count[1]: candidates with a view decision inside the guard
+//   band, re-scored by k_score_fix (numpy-order ctNcc) after the tiled kernel
 struct TiledArgs {
     int ntx, nty, ntiles;
+    int tw, th;                // tile size in pixels (x, y): 16x8 tiled kernels, 16x16 MFMA
     int chunk;                 // candidates per work item
     int32_t* tile_count;
     int32_t* tile_off;
@@ -70,6 +73,8 @@ struct TiledArgs {
     int32_t* cand_rank;
     int32_t* cand_pk;
     int2* sorted;
+    int32_t* fix_list;
+    int32_t* fix_count;
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).
@@ -106,14 +111,18 @@ struct ExpandArgs {
 extern "C" {
 int mvs_launch_build_stack(const uint8_t* d_rgb, uint8_t* d_stack, int V, int H, int W, int Wq,
                            hipStream_t s);
-int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s);
+// ev0/ev1 (may be null): recorded on s immediately before and after the
+// dominant scoring kernel (k_score / k_score_tiled3) -- kernel timing for bench.py
+int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s,
+                     hipEvent_t ev0, hipEvent_t ev1);
 int mvs_launch_build_gv(const uint8_t* d_stack, uint8_t* d_gv, int V, int H, int W, int Wq, int Wp,
                         hipStream_t s);
 int mvs_launch_build_moments(const SceneDev* sc, int wid, uint2* d_mom, hipStream_t s);
-// Tile geometry of the tiled scorer for a W x H image (so the host can size scratch).
-void mvs_tiled_geometry(int W, int H, int* ntx, int* nty);
+// Tile geometry of the tiled scorers for a W x H image (so the host can size
+// scratch): mfma != 0 -> the MFMA scorer's 16x16 tiles, else 16x8.
+void mvs_tiled_geometry(int W, int H, int mfma, int* tw, int* th, int* ntx, int* nty);
 int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
-                           int variant, hipStream_t s);
+                           int variant, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, int wid,
                       hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,

@@ -107,9 +107,11 @@ __device__ __forceinline__ double exact_ncc_stack(const SceneDev sc, int R, int 
 // lanes, then the four row sums combined from SGPRs.  Result in every lane.
 template <int CTRL>
 DEV double dpp_f64(double x) {
+    // bound_ctrl: every source lane of these patterns exists, so no "old" value
+    // (and no v_mov to materialise it) is needed
     const unsigned long long u = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, true);
     return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
@@ -524,7 +526,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             t.cand_key[i] = -1;
             continue;
         }
-        const int tile = (r / kTH) * t.ntx + (q / kTW);
+        const int tile = (r / t.th) * t.ntx + (q / t.tw);
         tl[k] = tile;
         t.cand_pk[i] = q | (r << 11) | (R << 22);
         lr[k] = atomicAdd(&hist[tile], 1);
@@ -813,6 +815,16 @@ DEV uint32_t sab_rows_smem(const uint32_t* own, cgu32* ref, int ref_pitch_dw) {
 
 constexpr int kT3Threads = 256, kT3Waves = kT3Threads / 64;
 
+// 1/k for k = 0..64 (entry 0 unused), correctly rounded at compile time:
+// avg_ncc_score = sum * (1/cnt) -- one multiply instead of a binary64 divide.
+struct RecipTable {
+    double r[65];
+    constexpr RecipTable() : r() {
+        for (int k = 1; k <= 64; ++k) r[k] = 1.0 / (double)k;
+    }
+};
+__constant__ constexpr RecipTable c_recip{};
+
 // Diagnostic build only (-DMVS_STAMPS): per-workgroup phase times of the
 // tiled kernel -- stage, candidates, write-out -- into a side buffer that no
 // output depends on.
@@ -829,8 +841,16 @@ __device__ unsigned long long g_stamps[4096 * 8];
             if ((k) == 3) g_stamps[blockIdx.x * 8] += 1;                                  \
         }                                                                                 \
     } while (0)
+// phase split inside the workgroup's loop (thread 0 = wave 0 only)
+#define STAMP_T(var) \
+    __builtin_amdgcn_sched_barrier(0); const unsigned long long var = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0)
+#define STAMP_ADD(k, t0, t1) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x * 8 + (k)] += (t1) - (t0); } while (0)
 #else
 #define STAMP(k) do { } while (0)
+#define STAMP_T(var) do { } while (0)
+#define STAMP_ADD(k, t0, t1) do { } while (0)
 #endif
 
 template <int WID, int QS, int REFSRC>
@@ -845,7 +865,9 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int V = sc.V;
     const int n_items = t.item_off[t.ntiles];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave index as an SGPR: the candidate loop, its SMEM loads and the
+    // alignment switch below are then scalar control flow
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint2* __restrict__ mom = sc.mom[WID];
     // output staging behind the region image (chunk <= kChunk candidates)
     uint64_t* o_mask = (uint64_t*)(lds + G::ROWS * RS);
@@ -860,7 +882,8 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
         // dynamic work queue: the next (tile, chunk) item for this workgroup
         if (threadIdx.x == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
         __syncthreads();
-        const int item = s_item;
+        // uniform from here on: tile bounds and offsets live in SGPRs
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
         if (item >= n_items) break;
         STAMP(0);
         int lo = 0, hi = t.ntiles;
@@ -957,44 +980,40 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
             const int32_t db = (int32_t)(__umul24(NPX, mb.y) - __umul24(mb.x, mb.x));
             const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma.x, mb.x));
             const bool live = lane < V && lane != R && da > 0 && db > 0;
-            bool pass = false;
+            bool pass = false, guard = false;
             double ncc = 0.0;
             if (live) {
                 if (a.thr >= 0.01) {
+                    // ncc > thr  <=>  L > 0 and L^2 > thr^2 (n-1)^2 da db, L = n*num
+                    // (exact in binary64); a relative band of 1e-8 around equality
+                    // goes to k_score_fix (numpy-order ctNcc)
                     const double L = (double)num * (double)NPX;
                     if (L > 0.0) {
                         const double tk = a.thr * (double)(NPX - 1);
                         const double rhs = (tk * tk) * ((double)da * (double)db);
                         const double diff = L * L - rhs;
-                        if (fabs(diff) <= 1e-8 * rhs) {
-                            ncc = exact_ncc_stack<WID>(sc, R, lane, q, r);
-                            atomicAdd(a.exact_hits, 1);
-                            pass = ncc > a.thr;
-                        } else {
-                            pass = diff > 0.0;
-                            if (pass && a.avg) {
-                                const double D = (double)da * (double)db;
-                                double y = __builtin_amdgcn_rsq(D);
-                                y = y * (1.5 - 0.5 * D * y * y);
-                                y = y * (1.5 - 0.5 * D * y * y);
-                                ncc = L * y * (1.0 / (double)(NPX - 1));
-                            }
+                        guard = fabs(diff) <= 1e-8 * rhs;
+                        pass = diff > 0.0;
+                        if (pass && a.avg) {
+                            const double D = (double)da * (double)db;
+                            double y = __builtin_amdgcn_rsq(D);
+                            y = y * (1.5 - 0.5 * D * y * y);
+                            y = y * (1.5 - 0.5 * D * y * y);
+                            ncc = L * y * (1.0 / (double)(NPX - 1));
                         }
                     }
                 } else {
                     ncc = ((double)num * (double)NPX) /
                           ((double)(NPX - 1) * sqrt((double)da * (double)db));
-                    if (fabs(ncc - a.thr) <= kGuard) {
-                        ncc = exact_ncc_stack<WID>(sc, R, lane, q, r);
-                        atomicAdd(a.exact_hits, 1);
-                    }
+                    guard = fabs(ncc - a.thr) <= kGuard;
                     pass = ncc > a.thr;
                 }
             }
+            if (__ballot(guard) != 0 && lane == 0) t.fix_list[atomicAdd(t.fix_count, 1)] = cur.x;
             const uint64_t m = __ballot(pass);
             const int cnt = __popcll(m);
             double avgv = 0.0;
-            if (a.avg && cnt) avgv = wave_sum_dpp(pass ? ncc : 0.0) / cnt;
+            if (a.avg && cnt) avgv = wave_sum_dpp(pass ? ncc : 0.0) * c_recip.r[cnt];
             const int slot = j - cb;
             if (lane == 0) {
                 o_mask[slot] = m;
@@ -1015,6 +1034,332 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
         }
         __syncthreads();
         STAMP(3);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// MFMA scorer.  S_ab of a candidate (pixel p, reference view R) against every
+// view v is a box sum over the window of the product image g_R * g_v.  For one
+// 16x16-pixel output tile and one R, all of them -- 16 x-positions x every
+// view x every output row -- come from one chain of
+// v_mfma_i32_16x16x64_i8 per 16-view slice: row y of the tile region
+// contributes  A_y(x, k) . B_y(k, v)  with A_y = g_R(y, k) masked to the band
+// x <= k - off0 <= x + 2 WID (the window's columns for output x) and
+// B_y = g_v(y, k); a running prefix over rows gives the vertical window sum
+// S_j = C_{j+2WID} - C_{j-1}.  Pixels are stored as g - 128 (signed bytes,
+// exact): sum (g_a-128)(g_b-128) = S_ab - 128 (S_a + S_b) + 16384 n.
+// Per candidate only the decision epilogue (moments, squared comparison,
+// avg) remains on the VALU, one lane per view as in k_score_tiled3.
+// ---------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int kMTW = 16, kMTH = 16;          // output tile (x, y)
+constexpr int kMThreads = 512, kMWaves = kMThreads / 64;
+constexpr int kMChunk = 1024;                // candidates per work item
+constexpr int kMNB = 16;                     // candidates per R pass (per-wave S buffer)
+
+template <int WID, int NT>
+struct MfmaGeom {
+    static constexpr int NB = 2 * WID + 1;
+    static constexpr int NR = kMTH + 2 * WID;     // region rows
+    static constexpr int VS = NR * 32 + 16;       // bytes per view: an odd number of 16-B units
+    static constexpr int NV = NT * 16;            // view slots
+    static constexpr int NKEY = 64 * kMTH;        // (R, output row) sort keys, V <= 64
+    static constexpr int OFF0 = (4 - WID % 4) % 4;   // window column of output x = x + OFF0
+    static_assert(kMTW + OFF0 + 2 * WID <= 32, "window must fit the 32 region columns");
+    static constexpr int O_REG = 0;
+    static constexpr int O_CU = (NV * VS + 15) / 16 * 16;             // int2[kMChunk] tile order
+    static constexpr int O_CS = O_CU + 8 * kMChunk;                    // int2[kMChunk] key order
+    static constexpr int O_HS = O_CS + 8 * kMChunk;                    // int[NKEY + 1] key starts
+    static constexpr int O_CUR = O_HS + 4 * (NKEY + 4);                // int[NKEY] counts/cursors
+    static constexpr int O_SB = O_CUR + 4 * NKEY;                      // int[waves][kMNB][64]
+    static constexpr int O_OM = O_SB + 4 * kMWaves * kMNB * 64;        // u64[kMChunk]
+    static constexpr int O_OA = O_OM + 8 * kMChunk;                    // double[kMChunk]
+    static constexpr int O_OC = O_OA + 8 * kMChunk;                    // int[kMChunk]
+    static constexpr int O_WT = O_OC + 4 * kMChunk;                    // int[kMWaves]
+    static constexpr int BYTES = O_WT + 4 * kMWaves;
+};
+
+template <int WID, int NT>
+__global__ __launch_bounds__(kMThreads, 2) void k_score_mfma(const SceneDev sc, const ScoreArgs a,
+                                                             const TiledArgs t) {
+    using G = MfmaGeom<WID, NT>;
+    constexpr int NB = G::NB, NPX = NB * NB, NR = G::NR, VS = G::VS;
+    constexpr int RING = NB + 1;              // prefixes C_{y-NB} .. C_y
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* reg = smem + G::O_REG;
+    int2* cu = (int2*)(smem + G::O_CU);
+    int2* cs = (int2*)(smem + G::O_CS);
+    int* hs = (int*)(smem + G::O_HS);
+    int* cur = (int*)(smem + G::O_CUR);
+    int* sbuf = (int*)(smem + G::O_SB);
+    uint64_t* o_mask = (uint64_t*)(smem + G::O_OM);
+    double* o_avg = (double*)(smem + G::O_OA);
+    int32_t* o_cnt = (int32_t*)(smem + G::O_OC);
+    int* wt = (int*)(smem + G::O_WT);
+    __shared__ int s_item;
+
+    const int V = sc.V;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n_items = t.item_off[t.ntiles];
+    const int nkey = V * kMTH;
+    const uint2* __restrict__ mom = sc.mom[WID];
+    const int lx = lane & 15, lh = lane >> 4;
+    // A-fragment band mask of this lane: output x = lx, region columns 16 lh + b
+    uint32_t bm[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int col = 16 * lh + 4 * d + b;
+            if (lh < 2 && col >= lx + G::OFF0 && col <= lx + G::OFF0 + 2 * WID) m |= 0xffu << (8 * b);
+        }
+        bm[d] = m;
+    }
+    int* my_sb = sbuf + wave * kMNB * 64;
+#ifdef MVS_STAMPS
+    unsigned long long st_prev = 0;
+#endif
+
+    for (;;) {
+        if (tid == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
+        __syncthreads();
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item >= n_items) break;
+        STAMP(0);
+        int lo = 0, hi = t.ntiles;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t.item_off[mid] <= item) lo = mid; else hi = mid;
+        }
+        const int tile = lo;
+        const int cb = t.tile_off[tile] + (item - t.item_off[tile]) * t.chunk;
+        const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
+        const int nc = ce - cb;
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int x0 = tx * kMTW, yo0 = ty * kMTH;
+        const int y0 = yo0 - WID;
+        const int kq0 = (x0 - WID) >> 2;          // floor
+        // ---- stage the region: NR rows x 8 quads x all views, as g ^ 0x80 ----
+        {
+            const int cpq = V >> 2, cpr = 8 * cpq, total = NR * cpr;
+            for (int base = 0; base < total; base += 4 * kMThreads) {
+                uint4 buf[4];
+                int dst[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = base + u * kMThreads + tid;
+                    dst[u] = -1;
+                    buf[u] = make_uint4(0, 0, 0, 0);
+                    if (k < total) {
+                        const int ry = k / cpr, rem = k - ry * cpr;
+                        const int kq = rem / cpq, vq = rem - kq * cpq;
+                        const int y = y0 + ry, gq = kq0 + kq;
+                        if (y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                            buf[u] = *(const uint4*)(sc.stack + (int64_t)y * sc.row_bytes +
+                                                      (int64_t)gq * V * 4 + vq * 16);
+                        dst[u] = (4 * vq) * VS + ry * 32 + kq * 4;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (dst[u] >= 0) {
+                        uint8_t* d = reg + dst[u];
+                        *(uint32_t*)(d) = buf[u].x ^ 0x80808080u;
+                        *(uint32_t*)(d + VS) = buf[u].y ^ 0x80808080u;
+                        *(uint32_t*)(d + 2 * VS) = buf[u].z ^ 0x80808080u;
+                        *(uint32_t*)(d + 3 * VS) = buf[u].w ^ 0x80808080u;
+                    }
+            }
+        }
+        // ---- candidates of the item, counting-sorted by (R, output row) ----
+        for (int k = tid; k < nkey; k += kMThreads) cur[k] = 0;
+        __syncthreads();
+        for (int k = tid; k < nc; k += kMThreads) {
+            const int2 e = t.sorted[cb + k];
+            cu[k] = e;
+            const int r = (e.y >> 11) & 0x7ff, R = (e.y >> 22) & 0x3ff;
+            atomicAdd(&cur[R * kMTH + (r - yo0)], 1);
+        }
+        __syncthreads();
+        {   // exclusive scan of cur[0 .. nkey) into hs (two keys per thread)
+            const int b = 2 * tid;
+            const int c0 = b < nkey ? cur[b] : 0, c1 = b + 1 < nkey ? cur[b + 1] : 0;
+            int sum = c0 + c1;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int u = __shfl_up(sum, off, 64);
+                if (lane >= off) sum += u;
+            }
+            if (lane == 63) wt[wave] = sum;
+            __syncthreads();
+            int before = 0;
+            for (int w = 0; w < wave; ++w) before += wt[w];
+            const int excl = before + sum - (c0 + c1);
+            if (b < nkey) { hs[b] = excl; cur[b] = excl; }
+            if (b + 1 < nkey) { hs[b + 1] = excl + c0; cur[b + 1] = excl + c0; }
+            if (tid == kMThreads - 1) hs[nkey] = before + sum;
+        }
+        __syncthreads();
+        for (int k = tid; k < nc; k += kMThreads) {
+            const int2 e = cu[k];
+            const int r = (e.y >> 11) & 0x7ff, R = (e.y >> 22) & 0x3ff;
+            cs[atomicAdd(&cur[R * kMTH + (r - yo0)], 1)] = e;
+        }
+        __syncthreads();
+        STAMP(1);
+        // ---- one reference view per wave at a time ----
+        for (int R = wave; R < V; R += kMWaves) {
+            const int gb = __builtin_amdgcn_readfirstlane(hs[R * kMTH]);
+            const int ge = __builtin_amdgcn_readfirstlane(hs[(R + 1) * kMTH]);
+            for (int pb = gb; pb < ge; pb += kMNB) {
+                const int pe = min(pb + kMNB, ge);
+                STAMP_T(tp0);
+                // moments of the pass's candidates, in flight during the MFMA rows
+                uint2 mbs[kMNB];
+#pragma unroll
+                for (int c = 0; c < kMNB; ++c) {
+                    mbs[c] = make_uint2(0, 0);
+                    if (pb + c < pe && lane < V) {
+                        const int pk = cs[pb + c].y;
+                        const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
+                        mbs[c] = mom[(r * sc.W + q) * V + lane];
+                    }
+                }
+                // MFMA rows: ring of prefixes C_y over the region rows
+                const uint8_t* ra = reg + R * VS + 16 * (lh & 1);
+                v4i C[RING][NT];
+#pragma unroll
+                for (int y = 0; y < NR; ++y) {
+                    const uint4 av = *(const uint4*)(ra + y * 32);
+                    const v4i A = {(int)(av.x & bm[0]), (int)(av.y & bm[1]), (int)(av.z & bm[2]),
+                                   (int)(av.w & bm[3])};
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        const uint4 bv = *(const uint4*)(reg + (16 * nt + lx) * VS + y * 32 + 16 * (lh & 1));
+                        const v4i B = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
+                        const v4i zero = {0, 0, 0, 0};
+                        C[y % RING][nt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                            A, B, y == 0 ? zero : C[(y + RING - 1) % RING][nt], 0, 0, 0);
+                    }
+                    if (y >= 2 * WID) {
+                        const int j = y - 2 * WID;   // output row
+                        const int kb = max(pb, __builtin_amdgcn_readfirstlane(hs[R * kMTH + j]));
+                        const int ke = min(pe, __builtin_amdgcn_readfirstlane(hs[R * kMTH + j + 1]));
+                        if (kb < ke) {
+                            v4i S[NT];
+#pragma unroll
+                            for (int nt = 0; nt < NT; ++nt)
+                                S[nt] = j == 0 ? C[y % RING][nt]
+                                               : C[y % RING][nt] - C[(y + 1) % RING][nt];  // C_{j-1} = C_{y-NB}
+                            for (int k = kb; k < ke; ++k) {
+                                const int pk = __builtin_amdgcn_readfirstlane(cs[k].y);
+                                const int x = (pk & 0x7ff) - x0;
+                                const int xi = x & 3;
+                                if (lh == (x >> 2)) {
+                                    int* d = my_sb + (k - pb) * 64 + lx;
+#pragma unroll
+                                    for (int nt = 0; nt < NT; ++nt) {
+                                        const int val = xi == 0 ? S[nt][0] : xi == 1 ? S[nt][1]
+                                                      : xi == 2 ? S[nt][2] : S[nt][3];
+                                        d[16 * nt] = val;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+                STAMP_T(tp1);
+                STAMP_ADD(4, tp0, tp1);
+                // decision epilogue: one lane per view, as k_score_tiled3
+                for (int k = pb; k < pe; ++k) {
+                    const int2 e = cs[k];
+                    const int ci = __builtin_amdgcn_readfirstlane(e.x);
+                    (void)ci;
+                    uint2 mb = mbs[0];
+#pragma unroll
+                    for (int c = 1; c < kMNB; ++c) mb = (k - pb == c) ? mbs[c] : mb;
+                    const uint2 ma = make_uint2(__builtin_amdgcn_readlane(mb.x, R),
+                                                __builtin_amdgcn_readlane(mb.y, R));
+                    const int sab_s = my_sb[(k - pb) * 64 + lane];
+                    const uint32_t Sab = (uint32_t)(sab_s + 128 * (int)(ma.x + mb.x) - 16384 * NPX);
+                    const int32_t da = (int32_t)(__umul24(NPX, ma.y) - __umul24(ma.x, ma.x));
+                    const int32_t db = (int32_t)(__umul24(NPX, mb.y) - __umul24(mb.x, mb.x));
+                    const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma.x, mb.x));
+                    const bool live = lane < V && lane != R && da > 0 && db > 0;
+                    bool pass = false, guard = false;
+                    double ncc = 0.0;
+                    if (live) {
+                        if (a.thr >= 0.01) {
+                            const double L = (double)num * (double)NPX;
+                            if (L > 0.0) {
+                                const double tk = a.thr * (double)(NPX - 1);
+                                const double rhs = (tk * tk) * ((double)da * (double)db);
+                                const double diff = L * L - rhs;
+                                guard = fabs(diff) <= 1e-8 * rhs;
+                                pass = diff > 0.0;
+                                if (pass && a.avg) {
+                                    const double D = (double)da * (double)db;
+                                    double yv = __builtin_amdgcn_rsq(D);
+                                    yv = yv * (1.5 - 0.5 * D * yv * yv);
+                                    yv = yv * (1.5 - 0.5 * D * yv * yv);
+                                    ncc = L * yv * (1.0 / (double)(NPX - 1));
+                                }
+                            }
+                        } else {
+                            ncc = ((double)num * (double)NPX) /
+                                  ((double)(NPX - 1) * sqrt((double)da * (double)db));
+                            guard = fabs(ncc - a.thr) <= kGuard;
+                            pass = ncc > a.thr;
+                        }
+                    }
+                    if (__ballot(guard) != 0 && lane == 0)
+                        t.fix_list[atomicAdd(t.fix_count, 1)] = e.x;
+                    const uint64_t m = __ballot(pass);
+                    const int cnt = __popcll(m);
+                    double avgv = 0.0;
+                    if (a.avg && cnt) avgv = wave_sum_dpp(pass ? ncc : 0.0) * c_recip.r[cnt];
+                    if (lane == 0) {
+                        o_mask[k] = m;
+                        o_avg[k] = avgv;
+                        o_cnt[k] = cnt;
+                    }
+                }
+                STAMP_T(tp2);
+                STAMP_ADD(5, tp1, tp2);
+                STAMP_ADD(6, 0, (unsigned long long)(pe - pb));
+            }
+        }
+        __syncthreads();
+        STAMP(2);
+        for (int k = tid; k < nc; k += kMThreads) {
+            const int i = cs[k].x;
+            a.mask[i] = o_mask[k];
+            a.count[i] = o_cnt[k];
+            if (a.avg) a.avg[i] = o_avg[k];
+        }
+        __syncthreads();
+        STAMP(3);
+    }
+}
+
+// Re-scores the candidates k_score_tiled3 flagged (a view decision inside the
+// guard band) with the direct scorer, whose guard lanes take the numpy-order
+// ctNcc; overwrites their mask/count/avg.  One wave per flagged candidate.
+template <int WID>
+__global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const ScoreArgs a,
+                                                   const TiledArgs t) {
+    const int nfix = *t.fix_count;
+    for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
+         k += gridDim.x * 4) {
+        const int64_t cand = __builtin_amdgcn_readfirstlane(t.fix_list[k]);
+        const int pk = __builtin_amdgcn_readfirstlane(t.cand_pk[cand]);
+        const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
+        wave_score<WID, 1>(sc, R, q, r, a.thr, a.mask + cand, a.count + cand,
+                           a.avg ? a.avg + cand : nullptr, a.exact_hits);
     }
 }
 
@@ -1145,10 +1490,25 @@ __global__ void k_ncc_windows(int64_t n, int npx, const uint8_t* __restrict__ A,
     }
 }
 
+// Records ev0 on construction and ev1 on destruction (when given): brackets
+// exactly one kernel launch on stream s.
+struct TimedLaunch {
+    hipStream_t s;
+    hipEvent_t e1;
+    TimedLaunch(hipStream_t s_, hipEvent_t e0, hipEvent_t e1_) : s(s_), e1(e1_) {
+        if (e0) (void)hipEventRecord(e0, s);
+    }
+    ~TimedLaunch() {
+        if (e1) (void)hipEventRecord(e1, s);
+    }
+};
+
 template <int WID>
-int launch_score_w(const SceneDev* sc, const ScoreArgs* a, hipStream_t s) {
+int launch_score_w(const SceneDev* sc, const ScoreArgs* a, hipStream_t s, hipEvent_t ev0,
+                   hipEvent_t ev1) {
     const int64_t blocks = (a->n + 3) / 4;
     if (blocks == 0) return 0;
+    TimedLaunch tl(s, ev0, ev1);
     if (sc->V <= 64)
         hipLaunchKernelGGL((k_score<WID, 1>), dim3((unsigned)blocks), dim3(256), 0, s, *sc, *a);
     else if (sc->V <= 128)
@@ -1158,12 +1518,19 @@ int launch_score_w(const SceneDev* sc, const ScoreArgs* a, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+template <int WID, int NT>
+void launch_mfma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s) {
+    constexpr size_t lds = MfmaGeom<WID, NT>::BYTES;
+    k_score_mfma<WID, NT><<<dim3(kTiledBlocks / 2), dim3(kMThreads), lds, s>>>(*sc, *a, *t);
+}
+
 template <int WID>
 int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int variant,
-                         hipStream_t s) {
+                         hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     using G = TileGeom<WID>;
     if (a->n == 0) return 0;
-    if (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 1), s) != hipSuccess) return -1;
+    // tile counters, the work-queue head (tile_count[ntiles]) and fix_count
+    if (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess) return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);
     hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
@@ -1171,10 +1538,28 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
     const size_t lds = (size_t)G::ROWS * G::NQ * 64 * 4;
+    if (variant == 6) {
+        if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kMChunk || t->th != kMTH ||
+            t->tw != kMTW)
+            return -3;
+        {
+            TimedLaunch tl(s, ev0, ev1);
+            switch ((sc->V + 15) / 16) {
+                case 1: launch_mfma<WID, 1>(sc, a, t, s); break;
+                case 2: launch_mfma<WID, 2>(sc, a, t, s); break;
+                case 3: launch_mfma<WID, 3>(sc, a, t, s); break;
+                default: launch_mfma<WID, 4>(sc, a, t, s); break;
+            }
+        }
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(64), dim3(256), 0, s, *sc, *a, *t);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (variant == 4 || variant == 5 || (variant == 0 && sc->mom[WID] != nullptr)) {
         if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kChunk) return -3;
         const size_t outs = (size_t)t->chunk * (8 + 8 + 4 + 4);
         const bool smem = variant == 4;
+        {
+        TimedLaunch tl(s, ev0, ev1);
         if (sc->V == 48 && variant != 5) {
             const size_t lds3 = (size_t)G::ROWS * G::NQ * 48 * 4 + outs;
             if (smem) hipLaunchKernelGGL((k_score_tiled3<WID, 48, 1>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
@@ -1184,8 +1569,11 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
             if (smem) hipLaunchKernelGGL((k_score_tiled3<WID, 64, 1>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
             else hipLaunchKernelGGL((k_score_tiled3<WID, 64, 0>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
         }
+        }
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(64), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+    TimedLaunch tl(s, ev0, ev1);
     switch (variant) {
         case 0: hipLaunchKernelGGL((k_score_tiled<WID, 2, 0>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
         case 1: hipLaunchKernelGGL((k_score_tiled<WID, 2, 1>), dim3(kTiledBlocks), dim3(256), lds, s, *sc, *a, *t); break;
@@ -1246,31 +1634,35 @@ extern "C" int mvs_launch_build_moments(const SceneDev* sc, int wid, uint2* d_mo
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s) {
+extern "C" int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s,
+                                hipEvent_t ev0, hipEvent_t ev1) {
     switch (wid) {
-        case 1: return launch_score_w<1>(sc, a, s);
-        case 2: return launch_score_w<2>(sc, a, s);
-        case 3: return launch_score_w<3>(sc, a, s);
-        case 4: return launch_score_w<4>(sc, a, s);
-        case 5: return launch_score_w<5>(sc, a, s);
+        case 1: return launch_score_w<1>(sc, a, s, ev0, ev1);
+        case 2: return launch_score_w<2>(sc, a, s, ev0, ev1);
+        case 3: return launch_score_w<3>(sc, a, s, ev0, ev1);
+        case 4: return launch_score_w<4>(sc, a, s, ev0, ev1);
+        case 5: return launch_score_w<5>(sc, a, s, ev0, ev1);
         default: return -2;
     }
 }
 
-extern "C" void mvs_tiled_geometry(int W, int H, int* ntx, int* nty) {
-    *ntx = (W + kTW - 1) / kTW;
-    *nty = (H + kTH - 1) / kTH;
+extern "C" void mvs_tiled_geometry(int W, int H, int mfma, int* tw, int* th, int* ntx, int* nty) {
+    *tw = mfma ? kMTW : kTW;
+    *th = mfma ? kMTH : kTH;
+    *ntx = (W + *tw - 1) / *tw;
+    *nty = (H + *th - 1) / *th;
 }
 
 extern "C" int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t,
-                                      int wid, int variant, hipStream_t s) {
+                                      int wid, int variant, hipStream_t s, hipEvent_t ev0,
+                                      hipEvent_t ev1) {
     if (sc->V > 64) return -3;
     switch (wid) {
-        case 1: return launch_score_tiled_w<1>(sc, a, t, variant, s);
-        case 2: return launch_score_tiled_w<2>(sc, a, t, variant, s);
-        case 3: return launch_score_tiled_w<3>(sc, a, t, variant, s);
-        case 4: return launch_score_tiled_w<4>(sc, a, t, variant, s);
-        case 5: return launch_score_tiled_w<5>(sc, a, t, variant, s);
+        case 1: return launch_score_tiled_w<1>(sc, a, t, variant, s, ev0, ev1);
+        case 2: return launch_score_tiled_w<2>(sc, a, t, variant, s, ev0, ev1);
+        case 3: return launch_score_tiled_w<3>(sc, a, t, variant, s, ev0, ev1);
+        case 4: return launch_score_tiled_w<4>(sc, a, t, variant, s, ev0, ev1);
+        case 5: return launch_score_tiled_w<5>(sc, a, t, variant, s, ev0, ev1);
         default: return -2;
     }
 }

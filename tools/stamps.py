@@ -9,7 +9,7 @@ pkg = importlib.import_module(bench.PKG_NAME)
 rgb, K, R, t = bench.load_scene()
 n = 1 << 20
 c, ref = pkg.synthetic.candidates(n, K, R, t, seed=0)
-ctx = pkg.MvsContext(rgb, K, R, t)
+ctx = pkg.MvsContext(rgb, K, R, t)   # MVS_VARIANT picks the kernel
 lib = pkg._lib.load()
 lib.mvs_read_stamps.argtypes = [ctypes.c_void_p]
 buf = np.zeros(4096 * 8, np.uint64)
@@ -24,4 +24,7 @@ act = items > 0
 print("workgroups with items:", act.sum(), "items:", items.sum())
 for k, name in [(1, "stage"), (2, "candidates"), (3, "write-out")]:
     print(f"{name:12s} mean per item {d[act, k].sum() / items.sum():10.0f} cycles   total per wg {d[act, k].mean():12.0f}")
+if d[:, 4].sum() > 0:
+    print(f"wave0 mfma rows  {d[act, 4].sum() / items.sum():10.0f} cycles per item; "
+          f"epilogue {d[act, 5].sum() / items.sum():10.0f}; wave0 candidates per item {d[act, 6].sum() / items.sum():.1f}")
 print("per-wg total", (d[act, 1] + d[act, 2] + d[act, 3]).mean(), "cycles; max", (d[act, 1] + d[act, 2] + d[act, 3]).max())
