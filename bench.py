@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--secondary-wid", type=int, default=3)
     ap.add_argument("--kernel", choices=["auto", "direct", "tiled"], default="auto",
                     help="scoring kernel (MVS_SCORE_KERNEL)")
+    ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
+                    help="dino: dinoRing 48x640x480 (SURVEY 8(d) config 2, the headline); "
+                         "ring256: synthetic 256x1920x1080 uniform-random textures (config 4)")
     a = ap.parse_args()
 
     import torch
@@ -80,10 +83,13 @@ def main():
     pkg = importlib.import_module(PKG_NAME)
     par = importlib.import_module(PKG_NAME + ".parallel")
 
-    rgb, K, R, t = load_scene()
-    V = len(rgb)
+    if a.scene == "dino":
+        rgb, K, R, t = load_scene()
+    else:
+        rgb, K, R, t = pkg.synthetic.ring_scene(256, 1080, 1920, seed=0)
+    V, H, W = rgb.shape[0], rgb.shape[1], rgb.shape[2]
     ctx = pkg.MvsContext(rgb, K, R, t, device=local)
-    c_np, ref_np = pkg.synthetic.candidates(a.n, K, R, t, seed=rank)
+    c_np, ref_np = pkg.synthetic.candidates(a.n, K, R, t, W=W, H=H, seed=rank)
     c = torch.from_numpy(c_np).to(dev)
     ref = torch.from_numpy(ref_np).to(dev)
     n = a.n
@@ -156,10 +162,15 @@ def main():
         sys.path.insert(0, os.path.join(REPO))
         from oracle import oracle as orc
         scene = orc.Scene(rgb, K, R, t)
-        m = min(a.cpu_sample, n)
+        m = min(a.cpu_sample * 48 // V, n)     # ~10 s of single-core work
         t0 = time.perf_counter()
         oxy, omask, ocount, _ = scene.score_batch(c_np[:m], ref_np[:m], a.thr, a.wid, nthreads=1)
         cdt = time.perf_counter() - t0
+        # the same sample on every host core (OpenMP), SURVEY 8(d) "CPU timing beside it"
+        ncores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 10**6))
+        t0 = time.perf_counter()
+        scene.score_batch(c_np[:m], ref_np[:m], a.thr, a.wid, nthreads=ncores)
+        cdt_all = time.perf_counter() - t0
         # the sample doubles as a parity spot check of the measured launch
         step(a.wid)
         torch.cuda.synchronize()
@@ -167,6 +178,7 @@ def main():
         cpu = {"value": m / cdt, "unit": "candidates/s", "cores": 1, "kind": "port",
                "sample": f"first {m} of the rank-0 sweep (same candidates, wid={a.wid}), "
                          f"oracle/mvs_oracle.c or_score_batch single-threaded, {cdt:.1f} s",
+               "value_all_cores": m / cdt_all, "cores_all": ncores,
                "parity_on_sample": bool(np.array_equal(cnt_gpu, ocount) and
                                         np.array_equal(mask[:m].cpu().numpy().view(np.uint64), omask))}
         if not cpu["parity_on_sample"]:
@@ -184,7 +196,9 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "candidate patches/sec NCC-scored (640×480, 48 views) at 1/2/4/8 MI355X; % HBM roofline",
+            "metric": ("candidate patches/sec NCC-scored (640×480, 48 views) at 1/2/4/8 MI355X; % HBM roofline"
+                       if a.scene == "dino" else
+                       "candidate patches/sec NCC-scored (1920×1080, 256 views, synthetic) at 1/2/4/8 MI355X; % HBM roofline"),
             "value": value,
             "unit": "candidates/s",
             "n_gpus": world,
@@ -195,8 +209,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "real dinoRing images (data/dinoRing) + synthetic candidate patches (seed = rank)",
-            "config": {"workload": f"dinoRing 48x640x480, one expansion sweep of {n} candidates per GPU, "
+            "data": ("real dinoRing images (data/dinoRing)" if a.scene == "dino" else
+                     "synthetic uniform-random textures (seed 0)") +
+                    " + synthetic candidate patches (seed = rank)",
+            "config": {"workload": f"{'dinoRing' if a.scene == 'dino' else 'ring'} {V}x{W}x{H}, "
+                                   f"one expansion sweep of {n} candidates per GPU, "
                                    f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
                                    f"MIN_NCC {a.thr}, accepted records all-gathered",
                        "global_batch": n * world, "wid": a.wid, "views": V,

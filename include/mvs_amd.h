@@ -35,6 +35,7 @@ extern "C" {
 
 typedef struct mvs_ctx mvs_ctx;
 typedef struct mvs_stage_result mvs_stage_result;
+typedef struct mvs_stage mvs_stage;
 
 /* Library version string. */
 const char* mvs_version(void);
@@ -112,6 +113,35 @@ int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows);
  * exact-path decisions. */
 int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats);
 void mvs_stage_free(mvs_stage_result* res);
+
+/* The same stage in steps, for several GPUs (one process and one context per
+ * GPU).  Every rank calls mvs_stage_begin with the same inputs
+ * and its (rank, world), then loops:
+ *   nj = mvs_stage_plan(st)          commit in reference order until the FIFO
+ *                                    head needs unscored children; plan the next
+ *                                    sweep of nj child jobs (0: stage finished)
+ *   mvs_stage_score_slice(st, out)   score this rank's contiguous slice of the
+ *                                    sweep (rank r: jobs [r*b + min(r, x),
+ *                                    ... + b + (r < x)), b = nj / world,
+ *                                    x = nj % world) and pack its records into
+ *                                    the device buffer out[ceil(nj/world)][width]
+ *                                    (world > 1; may be NULL when world == 1)
+ *   <all-gather the slices, e.g. RCCL>
+ *   mvs_stage_ingest(st, all)        all[world][ceil(nj/world)][width] (device):
+ *                                    every rank's records into the record table
+ * and ends with mvs_stage_finish (same result as mvs_stage_run) and
+ * mvs_stage_destroy.  width = mvs_stage_record_width(st) int64 words.  Seeding
+ * is replicated on every rank; the commit is identical on every rank because
+ * it reads identical records.  Calls are synchronous. */
+int mvs_stage_begin(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off,
+                    const int32_t* obs_view, const float* obs_xy, int cell_size, double scale,
+                    int wid, int64_t max_pops, int rank, int world, mvs_stage** out);
+int64_t mvs_stage_plan(mvs_stage* st);
+int mvs_stage_record_width(const mvs_stage* st);
+int mvs_stage_score_slice(mvs_stage* st, int64_t* d_out);
+int mvs_stage_ingest(mvs_stage* st, const int64_t* d_all);
+int mvs_stage_finish(mvs_stage* st, mvs_stage_result** out);
+void mvs_stage_destroy(mvs_stage* st);
 
 /* patch_expansion candidates (MVS2.py:329-369) for explicit jobs: job k =
  * (parent job_parent[k], hit view job_view[k], i = job_di[k] in {-1,+1}).

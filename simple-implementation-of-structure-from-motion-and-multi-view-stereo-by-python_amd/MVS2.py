@@ -81,14 +81,30 @@ def photo_consistency_batch(ctx, centroids, ref_views, MIN_NCC=0.7, wid=5):
 
 def DensePointsWithMVS2(imgs, global_set, args, max_pops=100000, device=None):
     """MVS2.py:176-295 on the GPU.  Returns None like the reference; the run's
-    counters are left in MVS2.last_stats."""
+    counters are left in MVS2.last_stats.
+
+    Under torch.distributed with world size > 1 (one process per GPU), the
+    expansion sweeps are sharded across ranks (parallel.stage_sharded); every
+    rank ends with the same patches and rank 0 writes the PLY files."""
     t0 = time.time()
     par_K, par_r, par_t = read_pars(args)
     n_observations, n_world_points, legal_sets = global_set.getInfo()
     track_off, obs_view, obs_xy = tracks_to_arrays(legal_sets)
     ctx = scene_context(imgs, par_K, par_r, par_t, device)
-    initial, allp, stats = ctx.stage(track_off, obs_view, obs_xy, cell_size=args.cell_size,
-                                     scale=args.scale, wid=5, max_pops=max_pops)
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    if world > 1:
+        from . import parallel
+        initial, allp, stats = parallel.stage_sharded(
+            ctx, track_off, obs_view, obs_xy, cell_size=args.cell_size, scale=args.scale, wid=5,
+            max_pops=max_pops, device=device)
+        if dist.get_rank() != 0:
+            last_stats.clear()
+            last_stats.update(stats)
+            return None
+    else:
+        initial, allp, stats = ctx.stage(track_off, obs_view, obs_xy, cell_size=args.cell_size,
+                                         scale=args.scale, wid=5, max_pops=max_pops)
     print("len of initial patches", len(initial))
     export2ply(initial[:, :3], initial[:, 3:], path="initial_patches")
     print("filter outliers")

@@ -41,6 +41,15 @@ SIGNATURES = [
     ("mvs_stage_run", ctypes.c_int, [_vp, ctypes.c_int64, _i64p, _i32p, _fp, ctypes.c_int,
                                      ctypes.c_double, ctypes.c_int, ctypes.c_int64,
                                      ctypes.POINTER(_vp)]),
+    ("mvs_stage_begin", ctypes.c_int, [_vp, ctypes.c_int64, _i64p, _i32p, _fp, ctypes.c_int,
+                                       ctypes.c_double, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                       ctypes.c_int, ctypes.POINTER(_vp)]),
+    ("mvs_stage_plan", ctypes.c_int64, [_vp]),
+    ("mvs_stage_record_width", ctypes.c_int, [_vp]),
+    ("mvs_stage_score_slice", ctypes.c_int, [_vp, _vp]),
+    ("mvs_stage_ingest", ctypes.c_int, [_vp, _vp]),
+    ("mvs_stage_finish", ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    ("mvs_stage_destroy", None, [_vp]),
     ("mvs_stage_count", ctypes.c_int64, [_vp, ctypes.c_int]),
     ("mvs_stage_rows", ctypes.c_int, [_vp, ctypes.c_int, _dp]),
     ("mvs_stage_stats", ctypes.c_int, [_vp, _i64p]),
@@ -237,29 +246,100 @@ class MvsContext:
     def stage(self, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5, max_pops=100000):
         """DensePointsWithMVS2 minus IO; returns (initial N0x6, all Nx6, stats dict)."""
         lib = load()
-        track_off = _c(track_off, np.int64)
-        obs_view = _c(obs_view, np.int32)
-        obs_xy = _c(obs_xy, np.float32).reshape(-1, 2)
+        track_off, obs_view, obs_xy = _tracks(track_off, obs_view, obs_xy)
         res = _vp()
         rc = lib.mvs_stage_run(self._h, len(track_off) - 1, _p(track_off, _i64p),
                                _p(obs_view, _i32p), _p(obs_xy, _fp), int(cell_size), float(scale),
                                int(wid), int(max_pops), ctypes.byref(res))
         check(rc, self._h, "mvs_stage_run")
+        return _take_result(res, self._h)
+
+    def stage_begin(self, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5,
+                    max_pops=100000, rank=0, world=1):
+        """The stage in steps (mvs_stage_begin ...); see parallel.stage_sharded."""
+        return Stage(self, track_off, obs_view, obs_xy, cell_size, scale, wid, max_pops, rank, world)
+
+
+STAGE_STATS = ["pops", "tests", "accepts", "queue_left", "scored", "sweeps", "seed_candidates",
+               "exact_hits"]
+
+
+def _tracks(track_off, obs_view, obs_xy):
+    return (_c(track_off, np.int64), _c(obs_view, np.int32),
+            _c(obs_xy, np.float32).reshape(-1, 2))
+
+
+def _take_result(res, h):
+    """Copy an mvs_stage_result out and free it -> (initial, all, stats)."""
+    lib = load()
+    try:
+        out = []
+        for which in (0, 1):
+            n = lib.mvs_stage_count(res, which)
+            rows = np.empty((n, 6))
+            if n:
+                check(lib.mvs_stage_rows(res, which, _p(rows, _dp)), h, "mvs_stage_rows")
+            out.append(rows)
+        st = np.empty(8, np.int64)
+        check(lib.mvs_stage_stats(res, _p(st, _i64p)), h, "mvs_stage_stats")
+    finally:
+        lib.mvs_stage_free(res)
+    return out[0], out[1], dict(zip(STAGE_STATS, (int(x) for x in st)))
+
+
+class Stage:
+    """One rank's view of a stepped stage run (include/mvs_amd.h, mvs_stage_*)."""
+
+    def __init__(self, ctx, track_off, obs_view, obs_xy, cell_size, scale, wid, max_pops, rank,
+                 world):
+        lib = load()
+        self.ctx = ctx
+        self.rank, self.world = int(rank), int(world)
+        self._tr = _tracks(track_off, obs_view, obs_xy)
+        h = _vp()
+        rc = lib.mvs_stage_begin(ctx.handle, len(self._tr[0]) - 1, _p(self._tr[0], _i64p),
+                                 _p(self._tr[1], _i32p), _p(self._tr[2], _fp), int(cell_size),
+                                 float(scale), int(wid), int(max_pops), self.rank, self.world,
+                                 ctypes.byref(h))
+        check(rc, ctx.handle, "mvs_stage_begin")
+        self._st = h
+        self.width = lib.mvs_stage_record_width(h)
+
+    def plan(self):
+        """Commit and plan the next sweep -> its job count (0: finished)."""
+        n = load().mvs_stage_plan(self._st)
+        if n < 0:
+            check(int(n), self.ctx.handle, "mvs_stage_plan")
+        return int(n)
+
+    def slice_max(self, nj):
+        return -(-nj // self.world)
+
+    def score_slice(self, out=None):
+        """Score this rank's slice; out = device int64 tensor (slice_max, width) when world > 1."""
+        ptr = out.data_ptr() if out is not None else None
+        check(load().mvs_stage_score_slice(self._st, ptr), self.ctx.handle, "mvs_stage_score_slice")
+
+    def ingest(self, gathered=None):
+        """gathered = device int64 tensor (world, slice_max, width) when world > 1."""
+        ptr = gathered.data_ptr() if gathered is not None else None
+        check(load().mvs_stage_ingest(self._st, ptr), self.ctx.handle, "mvs_stage_ingest")
+
+    def finish(self):
+        res = _vp()
+        check(load().mvs_stage_finish(self._st, ctypes.byref(res)), self.ctx.handle, "mvs_stage_finish")
+        return _take_result(res, self.ctx.handle)
+
+    def close(self):
+        if self._st:
+            load().mvs_stage_destroy(self._st)
+            self._st = None
+
+    def __del__(self):
         try:
-            out = []
-            for which in (0, 1):
-                n = lib.mvs_stage_count(res, which)
-                rows = np.empty((n, 6))
-                if n:
-                    check(lib.mvs_stage_rows(res, which, _p(rows, _dp)), self._h, "mvs_stage_rows")
-                out.append(rows)
-            st = np.empty(8, np.int64)
-            check(lib.mvs_stage_stats(res, _p(st, _i64p)), self._h, "mvs_stage_stats")
-        finally:
-            lib.mvs_stage_free(res)
-        keys = ["pops", "tests", "accepts", "queue_left", "scored", "sweeps", "seed_candidates",
-                "exact_hits"]
-        return out[0], out[1], dict(zip(keys, (int(x) for x in st)))
+            self.close()
+        except Exception:
+            pass
 
 
 def ncc_windows(a, b, thr, force_exact=False, stream=None):

@@ -308,6 +308,7 @@ struct mvs_ctx {
     int words() const { return (V + 63) / 64; }
 };
 
+struct mvs_stage;
 struct mvs_stage_result {
     std::vector<double> initial, all;
     int64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -652,104 +653,143 @@ struct Engine {
     double kmat(int v, int r, int c) const { return ctx->K[9 * v + 3 * r + c]; }
 
     // ---- patch_expansion: MVS2.py:308-404 ----
-    void expand() {
-        const bool trace = std::getenv("MVS_TRACE") != nullptr;
-        std::vector<int32_t> queue;
+    // The FIFO loop is split into steps so that several GPUs can share a
+    // sweep: plan() commits in reference order until the FIFO head needs
+    // children nobody has scored yet and lays out the next sweep's jobs;
+    // score_range() scores a contiguous slice of them into the record table;
+    // fetch_sweep() brings the sweep's gates to the host for the next plan().
+    // Every rank runs the same plan() on the same records, so all commits
+    // agree.
+    std::vector<int32_t> queue;
+    size_t qhead = 0;
+    std::vector<int32_t> unscored;   // records in order of first enqueue
+    size_t ucur = 0;
+    int64_t pops = 0;
+    std::vector<ChildJob> jobs;
+    int64_t sweep_first = 0, sweep_n = 0;
+    bool trace = false;
+
+    void expand_init() {
+        trace = std::getenv("MVS_TRACE") != nullptr;
+        queue.clear();
         queue.reserve(1 << 20);
-        size_t qhead = 0;
-        std::vector<int32_t> unscored;   // records in order of first enqueue
-        size_t ucur = 0;
+        qhead = 0;
+        unscored.clear();
+        ucur = 0;
+        pops = 0;
         for (int64_t r = 0; r < n_seeds; ++r) {
             queue.push_back((int32_t)r);
             unscored.push_back((int32_t)r);
             h_enq[r] = 1;
         }
-        int64_t pops = 0;
-        std::vector<ChildJob> jobs;
-        const double dist_thr = 0.05 / scale;
-        while (true) {
-            // ordered commit until the FIFO head has no scored children
-            while (qhead < queue.size() && pops < max_pops) {
-                const int32_t r = queue[qhead];
-                const int64_t base = h_child[r];
-                if (base < 0) break;
-                ++qhead;
-                ++pops;
-                const long ci = h_cell[2 * r], cj = h_cell[2 * r + 1];
-                int h = 0;
-                for (int w = 0; w < words; ++w) {
-                    uint64_t m = h_mask[(int64_t)r * words + w];
-                    while (m) {
-                        const int v = 64 * w + __builtin_ctzll(m);
-                        m &= m - 1;
-                        for (int i = -1; i <= 1; i += 2) {
-                            const int64_t child = base + 2 * h + (i > 0 ? 1 : 0);
-                            for (int j = -1; j <= 1; j += 2) {
-                                if (!vacant(v, ci + i, cj + j)) continue;
-                                ++stat_tests;
-                                if (trace) std::fprintf(stderr, "E pop %lld rec %d v %d i %d j %d child %lld acc %d cnt %d cell %d %d\n",
-                                    (long long)pops, r, v, i, j, (long long)child, (int)h_accept[child], h_count[child], h_cell[2*child], h_cell[2*child+1]);
-                                if (h_accept[child]) {
-                                    fill_record(child);
-                                    events.push_back((int32_t)child);
-                                    for (int k = 0; k < h_count[child]; ++k) queue.push_back((int32_t)child);
-                                    if (!h_enq[child]) {
-                                        h_enq[child] = 1;
-                                        unscored.push_back((int32_t)child);
-                                    }
-                                    break;
+    }
+
+    // Commit, then plan the next sweep; returns its job count (0: stage finished).
+    int64_t plan() {
+        // ordered commit until the FIFO head has no scored children
+        while (qhead < queue.size() && pops < max_pops) {
+            const int32_t r = queue[qhead];
+            const int64_t base = h_child[r];
+            if (base < 0) break;
+            ++qhead;
+            ++pops;
+            const long ci = h_cell[2 * r], cj = h_cell[2 * r + 1];
+            int h = 0;
+            for (int w = 0; w < words; ++w) {
+                uint64_t m = h_mask[(int64_t)r * words + w];
+                while (m) {
+                    const int v = 64 * w + __builtin_ctzll(m);
+                    m &= m - 1;
+                    for (int i = -1; i <= 1; i += 2) {
+                        const int64_t child = base + 2 * h + (i > 0 ? 1 : 0);
+                        for (int j = -1; j <= 1; j += 2) {
+                            if (!vacant(v, ci + i, cj + j)) continue;
+                            ++stat_tests;
+                            if (trace) std::fprintf(stderr, "E pop %lld rec %d v %d i %d j %d child %lld acc %d cnt %d cell %d %d\n",
+                                (long long)pops, r, v, i, j, (long long)child, (int)h_accept[child], h_count[child], h_cell[2*child], h_cell[2*child+1]);
+                            if (h_accept[child]) {
+                                fill_record(child);
+                                events.push_back((int32_t)child);
+                                for (int k = 0; k < h_count[child]; ++k) queue.push_back((int32_t)child);
+                                if (!h_enq[child]) {
+                                    h_enq[child] = 1;
+                                    unscored.push_back((int32_t)child);
                                 }
+                                break;
                             }
                         }
-                        ++h;
                     }
+                    ++h;
                 }
             }
-            if (qhead >= queue.size() || pops >= max_pops) break;
-            // sweep: score the children of the next unscored records
-            const int64_t remaining = max_pops - pops;
-            int64_t want = std::min<int64_t>(std::max<int64_t>(remaining / 4, 2048), 262144);
-            want = std::min<int64_t>(want, (int64_t)(unscored.size() - ucur));
-            jobs.clear();
-            const int64_t first = nrec;
-            for (int64_t k = 0; k < want; ++k) {
-                const int32_t r = unscored[ucur + k];
-                h_child[r] = first + (int64_t)jobs.size();
-                for (int w = 0; w < words; ++w) {
-                    uint64_t m = h_mask[(int64_t)r * words + w];
-                    while (m) {
-                        const int v = 64 * w + __builtin_ctzll(m);
-                        m &= m - 1;
-                        jobs.push_back(ChildJob{r, (int16_t)v, (int16_t)-1});
-                        jobs.push_back(ChildJob{r, (int16_t)v, (int16_t)1});
-                    }
-                }
-            }
-            ucur += want;
-            const int64_t nj = (int64_t)jobs.size();
-            reserve(nrec + nj);
-            d_jobs.ensure(nj);
-            if (nj) {
-                HIPCHK(hipMemcpyAsync(d_jobs.p, jobs.data(), nj * sizeof(ChildJob), hipMemcpyHostToDevice, s));
-                ExpandArgs a{};
-                a.n = nj;
-                a.first_out = first;
-                a.jobs = d_jobs.p;
-                a.cell_size = cs;
-                a.vlb = vlb;
-                a.dist_thr = dist_thr;
-                a.thr = 0.7;
-                a.exact_hits = ctx->d_exact.p;
-                if (mvs_launch_expand(&ctx->sc, recs(), &a, wid, s) != 0)
-                    throw Fail{MVS_E_HIP, "expand launch failed"};
-                nrec += nj;
-                fetch_range(first, nj);
-            }
-            stat_scored += nj;
-            stat_sweeps++;
         }
-        stat_pops = pops;
-        stat_queue_left = (int64_t)(queue.size() - qhead);
+        if (qhead >= queue.size() || pops >= max_pops) {
+            stat_pops = pops;
+            stat_queue_left = (int64_t)(queue.size() - qhead);
+            sweep_n = 0;
+            return 0;
+        }
+        // sweep: the children of the next unscored records (first-enqueue order)
+        const int64_t remaining = max_pops - pops;
+        int64_t want = std::min<int64_t>(std::max<int64_t>(remaining / 4, 2048), 262144);
+        want = std::min<int64_t>(want, (int64_t)(unscored.size() - ucur));
+        jobs.clear();
+        sweep_first = nrec;
+        for (int64_t k = 0; k < want; ++k) {
+            const int32_t r = unscored[ucur + k];
+            h_child[r] = sweep_first + (int64_t)jobs.size();
+            for (int w = 0; w < words; ++w) {
+                uint64_t m = h_mask[(int64_t)r * words + w];
+                while (m) {
+                    const int v = 64 * w + __builtin_ctzll(m);
+                    m &= m - 1;
+                    jobs.push_back(ChildJob{r, (int16_t)v, (int16_t)-1});
+                    jobs.push_back(ChildJob{r, (int16_t)v, (int16_t)1});
+                }
+            }
+        }
+        ucur += want;
+        sweep_n = (int64_t)jobs.size();
+        reserve(nrec + sweep_n);
+        d_jobs.ensure(sweep_n);
+        if (sweep_n)
+            HIPCHK(hipMemcpyAsync(d_jobs.p, jobs.data(), sweep_n * sizeof(ChildJob), hipMemcpyHostToDevice, s));
+        nrec += sweep_n;
+        stat_scored += sweep_n;
+        stat_sweeps++;
+        return sweep_n;
+    }
+
+    // k_expand over jobs [b, e) of the planned sweep -> records sweep_first + [b, e)
+    void score_range(int64_t b, int64_t e) {
+        if (e <= b) return;
+        ExpandArgs a{};
+        a.n = e - b;
+        a.first_out = sweep_first + b;
+        a.jobs = d_jobs.p + b;
+        a.cell_size = cs;
+        a.vlb = vlb;
+        a.dist_thr = 0.05 / scale;
+        a.thr = 0.7;
+        a.exact_hits = ctx->d_exact.p;
+        if (mvs_launch_expand(&ctx->sc, recs(), &a, wid, s) != 0) throw Fail{MVS_E_HIP, "expand launch failed"};
+    }
+
+    void fetch_sweep() { fetch_range(sweep_first, sweep_n); }
+
+    void expand() {
+        expand_init();
+        while (plan() > 0) {
+            score_range(0, sweep_n);
+            fetch_sweep();
+        }
+    }
+
+    // contiguous slice of n jobs for `rank` (sizes differ by <= 1; parallel.shard_range)
+    static void shard(int64_t n, int rank, int world, int64_t* b, int64_t* e) {
+        const int64_t base = n / world, extra = n % world;
+        *b = rank * base + std::min<int64_t>(rank, extra);
+        *e = *b + base + (rank < extra ? 1 : 0);
     }
     int64_t stat_pops = 0, stat_queue_left = 0;
 
@@ -794,6 +834,41 @@ struct Engine {
     }
 };
 
+}  // namespace
+
+struct mvs_stage {
+    mvs_ctx* ctx = nullptr;
+    std::unique_ptr<Engine> E;
+    int rank = 0, world = 1;
+    int stage_state = 0;   // 0 planned nothing, 1 sweep planned, 2 slice scored, 3 finished
+};
+
+namespace {
+Engine* make_engine(mvs_ctx* ctx, int cell_size, double scale, int wid, int64_t max_pops) {
+    std::unique_ptr<Engine> E(new Engine());
+    E->ctx = ctx;
+    E->V = ctx->V;
+    E->words = ctx->words();
+    E->cs = cell_size;
+    E->wid = wid;
+    E->vlb = ctx->V > 2 ? 3 : 2;   // MVS2.py:200-203
+    E->scale = scale;
+    // CellTable: ceil((W-1)/cs) x ceil((H-1)/cs) per view (MVS2.py:88)
+    E->nci = (int)std::ceil((double)(ctx->W - 1) / cell_size);
+    E->ncj = (int)std::ceil((double)(ctx->H - 1) / cell_size);
+    E->max_pops = std::min<int64_t>(std::max<int64_t>(max_pops, 0), 100000);   // MVS2.py:321
+    E->s = ctx->stream;
+    E->table.assign((size_t)ctx->V * E->nci * E->ncj, 1);
+    return E.release();
+}
+
+void finish_engine(mvs_ctx* ctx, Engine* E, mvs_stage_result* res) {
+    E->output(res);
+    int32_t h = 0;
+    HIPCHK(hipMemcpyAsync(&h, ctx->d_exact.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    res->stats[7] = h;
+}
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -975,31 +1050,120 @@ int mvs_stage_run(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off, cons
     *out = nullptr;
     return guarded(ctx, [&]() {
         std::unique_ptr<mvs_stage_result> res(new mvs_stage_result());
-        std::unique_ptr<Engine> E(new Engine());
-        E->ctx = ctx;
-        E->V = ctx->V;
-        E->words = ctx->words();
-        E->cs = cell_size;
-        E->wid = wid;
-        E->vlb = ctx->V > 2 ? 3 : 2;   // MVS2.py:200-203
-        E->scale = scale;
-        // CellTable: ceil((W-1)/cs) x ceil((H-1)/cs) per view (MVS2.py:88)
-        E->nci = (int)std::ceil((double)(ctx->W - 1) / cell_size);
-        E->ncj = (int)std::ceil((double)(ctx->H - 1) / cell_size);
-        E->max_pops = std::min<int64_t>(std::max<int64_t>(max_pops, 0), 100000);   // MVS2.py:321
-        E->s = ctx->stream;
-        E->table.assign((size_t)ctx->V * E->nci * E->ncj, 1);
+        std::unique_ptr<Engine> E(make_engine(ctx, cell_size, scale, wid, max_pops));
         HIPCHK(hipMemsetAsync(ctx->d_exact.p, 0, sizeof(int32_t), ctx->stream));
         E->seed(n_tracks, track_off, obs_view, obs_xy);
         E->expand();
-        E->output(res.get());
-        int32_t h = 0;
-        HIPCHK(hipMemcpyAsync(&h, ctx->d_exact.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        res->stats[7] = h;
+        finish_engine(ctx, E.get(), res.get());
         *out = res.release();
         return 0;
     });
+}
+
+int mvs_stage_begin(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off, const int32_t* obs_view,
+                    const float* obs_xy, int cell_size, double scale, int wid, int64_t max_pops,
+                    int rank, int world, mvs_stage** out) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (!out || n_tracks < 0 || (n_tracks > 0 && (!track_off || !obs_view || !obs_xy)) || cell_size < 1 ||
+        world < 1 || rank < 0 || rank >= world)
+        return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
+    if (wid != 3 && wid != 5) return set_err(ctx, Fail{MVS_E_UNSUPPORTED, "stage supports wid 3 or 5"});
+    *out = nullptr;
+    return guarded(ctx, [&]() {
+        std::unique_ptr<mvs_stage> st(new mvs_stage());
+        st->ctx = ctx;
+        st->rank = rank;
+        st->world = world;
+        st->E.reset(make_engine(ctx, cell_size, scale, wid, max_pops));
+        HIPCHK(hipMemsetAsync(ctx->d_exact.p, 0, sizeof(int32_t), ctx->stream));
+        // seeding is replicated: every rank scores the (small) seed batch itself
+        st->E->seed(n_tracks, track_off, obs_view, obs_xy);
+        st->E->expand_init();
+        *out = st.release();
+        return 0;
+    });
+}
+
+int64_t mvs_stage_plan(mvs_stage* st) {
+    if (!st) return set_err(nullptr, Fail{MVS_E_ARG, "null stage"});
+    if (st->stage_state == 1 || st->stage_state == 2)
+        return set_err(st->ctx, Fail{MVS_E_ARG, "mvs_stage_plan: previous sweep not ingested"});
+    if (st->stage_state == 3) return 0;
+    int64_t nj = 0;
+    const int rc = guarded(st->ctx, [&]() {
+        nj = st->E->plan();
+        return 0;
+    });
+    if (rc) return rc;
+    st->stage_state = nj > 0 ? 1 : 3;
+    return nj;
+}
+
+int mvs_stage_record_width(const mvs_stage* st) {
+    if (!st) return MVS_E_ARG;
+    return 8 + st->E->words + 3;
+}
+
+int mvs_stage_score_slice(mvs_stage* st, int64_t* d_out) {
+    if (!st) return set_err(nullptr, Fail{MVS_E_ARG, "null stage"});
+    if (st->stage_state != 1) return set_err(st->ctx, Fail{MVS_E_ARG, "mvs_stage_score_slice: no planned sweep"});
+    if (st->world > 1 && !d_out) return set_err(st->ctx, Fail{MVS_E_ARG, "null slice buffer"});
+    const int rc = guarded(st->ctx, [&]() {
+        Engine* E = st->E.get();
+        int64_t b, e;
+        Engine::shard(E->sweep_n, st->rank, st->world, &b, &e);
+        E->score_range(b, e);
+        if (st->world > 1 &&
+            mvs_launch_pack_records(E->recs(), E->words, E->sweep_first + b, e - b, d_out, E->s) != 0)
+            throw Fail{MVS_E_HIP, "pack launch failed"};
+        HIPCHK(hipStreamSynchronize(E->s));
+        return 0;
+    });
+    if (rc == 0) st->stage_state = 2;
+    return rc;
+}
+
+int mvs_stage_ingest(mvs_stage* st, const int64_t* d_all) {
+    if (!st) return set_err(nullptr, Fail{MVS_E_ARG, "null stage"});
+    if (st->stage_state != 2) return set_err(st->ctx, Fail{MVS_E_ARG, "mvs_stage_ingest: slice not scored"});
+    if (st->world > 1 && !d_all) return set_err(st->ctx, Fail{MVS_E_ARG, "null gathered buffer"});
+    const int rc = guarded(st->ctx, [&]() {
+        Engine* E = st->E.get();
+        if (st->world > 1) {
+            const int64_t smax = (E->sweep_n + st->world - 1) / st->world;
+            const int64_t w = 8 + E->words + 3;
+            for (int r = 0; r < st->world; ++r) {
+                if (r == st->rank) continue;   // own slice is already in the record table
+                int64_t b, e;
+                Engine::shard(E->sweep_n, r, st->world, &b, &e);
+                if (mvs_launch_unpack_records(E->recs(), E->words, E->sweep_first + b, e - b,
+                                              d_all + (int64_t)r * smax * w, E->s) != 0)
+                    throw Fail{MVS_E_HIP, "unpack launch failed"};
+            }
+        }
+        E->fetch_sweep();
+        return 0;
+    });
+    if (rc == 0) st->stage_state = 0;
+    return rc;
+}
+
+int mvs_stage_finish(mvs_stage* st, mvs_stage_result** out) {
+    if (!st || !out) return set_err(st ? st->ctx : nullptr, Fail{MVS_E_ARG, "bad arguments"});
+    if (st->stage_state != 3) return set_err(st->ctx, Fail{MVS_E_ARG, "mvs_stage_finish: stage not finished"});
+    *out = nullptr;
+    return guarded(st->ctx, [&]() {
+        std::unique_ptr<mvs_stage_result> res(new mvs_stage_result());
+        finish_engine(st->ctx, st->E.get(), res.get());
+        *out = res.release();
+        return 0;
+    });
+}
+
+void mvs_stage_destroy(mvs_stage* st) {
+    if (!st) return;
+    if (st->ctx) (void)hipSetDevice(st->ctx->device);
+    delete st;
 }
 
 int64_t mvs_stage_count(const mvs_stage_result* res, int which) {

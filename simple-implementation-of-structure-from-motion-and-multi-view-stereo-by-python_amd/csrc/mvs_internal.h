@@ -125,6 +125,12 @@ int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledAr
                            int variant, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, int wid,
                       hipStream_t s);
+// Packed record rows for the multi-GPU stage exchange: int64 words
+// [c0 c1 c2 n0 n1 n2 x y | mask[words] | R + count<<32 | cell0 + cell1<<32 | rgba + accept<<32]
+int mvs_launch_pack_records(RecordsDev rec, int words, int64_t first, int64_t n, int64_t* out,
+                            hipStream_t s);
+int mvs_launch_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n,
+                              const int64_t* in, hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
                            int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
 }

@@ -1676,6 +1676,62 @@ extern "C" int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const Expan
     }
 }
 
+namespace {
+__global__ void k_pack_records(RecordsDev rec, int words, int64_t first, int64_t n, int64_t* out) {
+    const int w = 8 + words + 3;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = first + k;
+        int64_t* o = out + k * w;
+        for (int q = 0; q < 3; ++q) o[q] = __double_as_longlong(rec.c[3 * r + q]);
+        for (int q = 0; q < 3; ++q) o[3 + q] = __double_as_longlong(rec.n[3 * r + q]);
+        o[6] = __double_as_longlong(rec.xy[2 * r]);
+        o[7] = __double_as_longlong(rec.xy[2 * r + 1]);
+        for (int q = 0; q < words; ++q) o[8 + q] = (int64_t)rec.mask[r * words + q];
+        o[8 + words] = (int64_t)(uint32_t)rec.R[r] | ((int64_t)(uint32_t)rec.count[r] << 32);
+        o[9 + words] = (int64_t)(uint32_t)rec.cell[2 * r] | ((int64_t)(uint32_t)rec.cell[2 * r + 1] << 32);
+        const uint32_t rgba = *(const uint32_t*)(rec.color + 4 * r);
+        o[10 + words] = (int64_t)rgba | ((int64_t)rec.accept[r] << 32);
+    }
+}
+
+__global__ void k_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n, const int64_t* in) {
+    const int w = 8 + words + 3;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = first + k;
+        const int64_t* o = in + k * w;
+        for (int q = 0; q < 3; ++q) rec.c[3 * r + q] = __longlong_as_double(o[q]);
+        for (int q = 0; q < 3; ++q) rec.n[3 * r + q] = __longlong_as_double(o[3 + q]);
+        rec.xy[2 * r] = __longlong_as_double(o[6]);
+        rec.xy[2 * r + 1] = __longlong_as_double(o[7]);
+        for (int q = 0; q < words; ++q) rec.mask[r * words + q] = (uint64_t)o[8 + q];
+        rec.R[r] = (int32_t)(uint32_t)o[8 + words];
+        rec.count[r] = (int32_t)(uint32_t)((uint64_t)o[8 + words] >> 32);
+        rec.cell[2 * r] = (int32_t)(uint32_t)o[9 + words];
+        rec.cell[2 * r + 1] = (int32_t)(uint32_t)((uint64_t)o[9 + words] >> 32);
+        *(uint32_t*)(rec.color + 4 * r) = (uint32_t)o[10 + words];
+        rec.accept[r] = (uint8_t)((uint64_t)o[10 + words] >> 32);
+    }
+}
+}  // namespace
+
+extern "C" int mvs_launch_pack_records(RecordsDev rec, int words, int64_t first, int64_t n,
+                                       int64_t* out, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_pack_records, dim3(blocks), dim3(256), 0, s, rec, words, first, n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mvs_launch_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n,
+                                         const int64_t* in, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_unpack_records, dim3(blocks), dim3(256), 0, s, rec, words, first, n, in);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b,
                                       double thr, int force_exact, double* ncc, uint8_t* pass,
                                       hipStream_t s) {

@@ -11,6 +11,12 @@ rank holds the sweep's accepted set -- the input of the replicated,
 order-deterministic commit.
 
 Record layout (int64 columns): [global index, count, mask words..., x bits, y bits].
+
+stage_sharded() runs the whole DensePointsWithMVS2 stage this way: every
+expansion sweep (the children of a block of queued patches, MVS2.py:329-369)
+is split into contiguous per-rank slices, each rank scores its slice on its
+GPU, the packed records are all-gathered, and every rank runs the identical
+ordered commit (mvs_stage_* in include/mvs_amd.h).
 """
 import torch
 import torch.distributed as dist
@@ -78,3 +84,44 @@ def sharded_sweep(score_fn, c, ref, vlb, words, group=None):
     rec = pack_accepted(b, count, mask, xy, vlb)
     allrec = all_gather_records(rec, group) if world > 1 else rec
     return unpack_records(allrec, words)
+
+
+def gather_slices(out, group=None):
+    """All-gather equal-size slice blocks (slice_max, width) -> (world, slice_max, width)."""
+    world = dist.get_world_size(group)
+    # concatenated along dim 0 (the layout every backend accepts), viewed per rank
+    flat = torch.empty((world * out.shape[0],) + tuple(out.shape[1:]), dtype=out.dtype,
+                       device=out.device)
+    dist.all_gather_into_tensor(flat, out.contiguous(), group=group)
+    return flat.view((world,) + tuple(out.shape))
+
+
+def stage_sharded(ctx, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5,
+                  max_pops=100000, group=None, device=None):
+    """DensePointsWithMVS2 minus IO on every rank of `group` (one GPU each).
+
+    Returns the same (initial, all, stats) on every rank as MvsContext.stage()
+    returns on one GPU."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if device is None:
+        device = torch.device("cuda", int(ctx.device))
+    st = ctx.stage_begin(track_off, obs_view, obs_xy, cell_size, scale, wid, max_pops, rank, world)
+    try:
+        while True:
+            nj = st.plan()
+            if nj == 0:
+                break
+            if world == 1:
+                st.score_slice(None)
+                st.ingest(None)
+                continue
+            out = torch.empty((st.slice_max(nj), st.width), dtype=torch.int64, device=device)
+            st.score_slice(out)          # synchronous on the library's stream
+            allbuf = gather_slices(out, group)
+            if allbuf.is_cuda:
+                torch.cuda.current_stream(device).synchronize()
+            st.ingest(allbuf)
+        return st.finish()
+    finally:
+        st.close()

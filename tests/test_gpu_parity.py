@@ -329,3 +329,77 @@ def test_main_entry_point(pkg, tmp_path, monkeypatch):
     g = stage_golden(200)
     assert np.array_equal(pkg.read_ply(str(tmp_path / "initial_patches.ply")), g["initial_patches"])
     assert np.array_equal(pkg.read_ply(str(tmp_path / "all_patches.ply")), g["all_patches"])
+
+
+def _full_fixture():
+    import json
+    import os
+    from conftest import GOLDEN
+    p = os.path.join(GOLDEN, "stage_oracle_cap100000.json")
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+def test_stage_stepped_single_rank_matches_run(pkg, ctx, seeds):
+    """parallel.stage_sharded with one rank (the stepped C-ABI, mvs_stage_*)
+    gives exactly mvs_stage_run's patches and counters."""
+    import importlib
+    par = importlib.import_module(pkg.__name__ + ".parallel")
+    args = (seeds["track_off"], seeds["obs_view"], seeds["obs_xy"])
+    ini, allp, st = ctx.stage(*args, cell_size=2, scale=10.0, wid=5, max_pops=20000)
+    ini2, allp2, st2 = par.stage_sharded(ctx, *args, cell_size=2, scale=10.0, wid=5, max_pops=20000)
+    assert np.array_equal(ini, ini2) and np.array_equal(allp, allp2)
+    assert st == st2
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_stage_sharded_ranks_emulated(pkg, dino, seeds, world):
+    """The multi-GPU stage protocol with `world` ranks emulated in one process
+    (one context per rank on cuda:0): every sweep is split into per-rank
+    slices, each rank scores only its slice, the packed slices are stacked as
+    the all-gather would deliver them, every rank ingests them.  Each rank must
+    end with the single-GPU result; at the reference's full 100,000 pops it
+    must match the oracle fixture."""
+    import hashlib
+    import torch
+    rgb, K, R, t = dino
+    args = (seeds["track_off"], seeds["obs_view"], seeds["obs_xy"])
+    ctxs = [pkg.MvsContext(rgb, K, R, t, device=0) for _ in range(world)]
+    try:
+        sts = [c.stage_begin(*args, cell_size=2, scale=10.0, wid=5, max_pops=100000, rank=r,
+                             world=world) for r, c in enumerate(ctxs)]
+        dev = torch.device("cuda", 0)
+        sweeps = 0
+        while True:
+            njs = [s.plan() for s in sts]
+            assert len(set(njs)) == 1, njs
+            nj = njs[0]
+            if nj == 0:
+                break
+            sweeps += 1
+            smax = sts[0].slice_max(nj)
+            outs = [torch.full((smax, sts[0].width), -7, dtype=torch.int64, device=dev)
+                    for _ in range(world)]
+            for s, o in zip(sts, outs):
+                s.score_slice(o)
+            allbuf = torch.stack(outs)
+            for s in sts:
+                s.ingest(allbuf)
+        res = [s.finish() for s in sts]
+        for s in sts:
+            s.close()
+    finally:
+        for c in ctxs:
+            c.close()
+    ref_ctx = pkg.MvsContext(rgb, K, R, t, device=0)
+    ini, allp, st = ref_ctx.stage(*args, cell_size=2, scale=10.0, wid=5, max_pops=100000)
+    ref_ctx.close()
+    assert sweeps == st["sweeps"]
+    for ini_r, allp_r, st_r in res:
+        assert np.array_equal(ini_r, ini) and np.array_equal(allp_r, allp)
+        for k in ("pops", "tests", "accepts", "queue_left", "scored", "sweeps"):
+            assert st_r[k] == st[k]
+    j = _full_fixture()
+    if j is not None:
+        ini_r, allp_r, st_r = res[-1]
+        assert st_r["tests"] == j["stats"]["tests"]
+        assert hashlib.sha256(np.ascontiguousarray(allp_r, "<f8").tobytes()).hexdigest() == j["sha256_all"]
