@@ -5,7 +5,10 @@
 
 The MVS stage (DensePointsWithMVS2, MVS2.py:176) runs on the GPU through
 libmvs_amd.so and writes initial_patches.ply / all_patches.ply in the working
-directory, like the reference.  The reference's SfM stage (ORB + FLANN +
+directory, like the reference.  Under torchrun (one process per GPU) the
+expansion sweeps are sharded over the GPUs:
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py -img_p ... -seeds ...  The reference's SfM stage (ORB + FLANN +
 RANSAC through OpenCV, SFM.py) is not part of this build: its output -- the
 GlobalSet tracks -- is read from -seeds (npz with track_off, obs_view, obs_xy,
 the format tests/golden/make_seeds.py writes).
@@ -22,13 +25,24 @@ sys.path.insert(0, REPO)
 
 def main(args):
     mvs = importlib.import_module(PKG_NAME)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        # one process per GPU (torchrun): the expansion sweeps are sharded over
+        # the ranks and exchanged with RCCL (parallel.stage_sharded)
+        import torch
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     imgs = mvs.read_imgs(args)
     if not args.seeds:
         raise RuntimeError("no SfM tracks: this build has no OpenCV SfM stage; pass -seeds FILE.npz")
     global_set = mvs.SeedSet.load(args.seeds)
     mvs.DensePointsWithMVS2(imgs, global_set, args, max_pops=args.max_pops)
     st = mvs.MVS2.last_stats
-    print("pops {pops} tests {tests} accepted {accepts} gpu-scored {scored} sweeps {sweeps}".format(**st))
+    if world == 1 or int(os.environ.get("RANK", "0")) == 0:
+        print("pops {pops} tests {tests} accepted {accepts} gpu-scored {scored} sweeps {sweeps}".format(**st))
 
 
 if __name__ == "__main__":
