@@ -752,18 +752,28 @@ struct QuadMasks {
     }
 };
 
+using lds_u32 = __attribute__((address_space(3))) const uint32_t;
+
 template <int WID, int O, int RS, int QS>
-DEV uint32_t sab_rows(const uint32_t* own, const uint32_t* ref) {
+DEV uint32_t sab_rows(const uint32_t* own_g, const uint32_t* ref_g) {
     using M = QuadMasks<WID, O>;
     constexpr int NB = 2 * WID + 1;
     uint32_t d[NB][M::NQ], e[NB][M::NQ];
 #pragma unroll
-    for (int row = 0; row < NB; ++row)
+    for (int jj = 0; jj < M::NQ; ++jj) {
+        // one base register per quad column: the rows are RS dwords apart (a
+        // multiple of 64 when RS = 8*48), so each column's 11 rows pair up
+        // into ds_read2st64_b32 off that base with no further address math
+        lds_u32* o = (lds_u32*)own_g + jj * QS;
+        lds_u32* r = (lds_u32*)ref_g + jj * QS;
+        asm volatile("" : "+v"(o));
+        asm volatile("" : "+v"(r));
 #pragma unroll
-        for (int jj = 0; jj < M::NQ; ++jj) {
-            d[row][jj] = own[row * RS + jj * QS];
-            e[row][jj] = ref[row * RS + jj * QS];
+        for (int row = 0; row < NB; ++row) {
+            d[row][jj] = o[row * RS];
+            e[row][jj] = r[row * RS];
         }
+    }
     uint32_t ab[M::NQ];
 #pragma unroll
     for (int jj = 0; jj < M::NQ; ++jj) ab[jj] = 0;
@@ -771,8 +781,6 @@ DEV uint32_t sab_rows(const uint32_t* own, const uint32_t* ref) {
     for (int row = 0; row < NB; ++row)
 #pragma unroll
         for (int jj = 0; jj < M::NQ; ++jj) {
-            constexpr uint32_t dummy = 0;
-            (void)dummy;
             const uint32_t m = M::mask(jj);
             const uint32_t am = (m == 0xffffffffu) ? e[row][jj] : (e[row][jj] & m);
             ab[jj] = __builtin_amdgcn_udot4(am, d[row][jj], ab[jj], false);
