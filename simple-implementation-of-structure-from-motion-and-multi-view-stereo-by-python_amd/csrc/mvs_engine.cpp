@@ -272,7 +272,7 @@ struct mvs_ctx {
     std::vector<double> K;   // V*9 as given (getProjectionMatrix uses all of K)
     std::vector<uint8_t> h_rgb;
     DevBuf<uint8_t> d_rgb, d_stack, d_gv;
-    DevBuf<uint2> d_mom[MVS_MAX_WID + 1];
+    DevBuf<MomEntry> d_mom[MVS_MAX_WID + 1];
     DevBuf<CamDev> d_cams;
     DevBuf<int32_t> d_exact;
     SceneDev sc{};
@@ -379,8 +379,8 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
     a.exact_hits = ctx->d_exact.p;
     const bool tiled = ctx->V <= 64 && (ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048));
     // the MFMA scorer stages 16-B groups of 4 views: other view counts take the 16x8 tiled path
-    const int variant = (ctx->variant == 6 && (ctx->V & 3) != 0) ? 0 : ctx->variant;
-    if (tiled && (variant == 4 || variant == 5 || variant == 6 || variant == 0) && (ctx->V & 3) == 0 &&
+    const int variant = ((ctx->variant == 6 || ctx->variant == 9) && (ctx->V & 3) != 0) ? 0 : ctx->variant;
+    if (tiled && (variant == 0 || variant >= 4) && (ctx->V & 3) == 0 &&
         !ctx->sc.mom[wid]) {
         // scene moments for this window size: built once, reused by every batch
         ctx->d_mom[wid].alloc((size_t)ctx->H * ctx->W * ctx->V);
@@ -396,7 +396,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         ctx->t_tiles.ensure((size_t)3 * (ntiles + 2));
         ctx->t_cand.ensure((size_t)6 * n);
         t.ntiles = ntiles;
-        t.chunk = mfma ? 1024 : (variant == 0 || variant >= 4) ? ctx->chunk3 : 512;
+        t.chunk = mfma ? 1024 : variant == 9 ? 256 : (variant == 0 || variant >= 4) ? ctx->chunk3 : 512;
         t.tile_count = ctx->t_tiles.p;
         t.tile_off = ctx->t_tiles.p + (ntiles + 2);
         t.item_off = ctx->t_tiles.p + 2 * (ntiles + 2);

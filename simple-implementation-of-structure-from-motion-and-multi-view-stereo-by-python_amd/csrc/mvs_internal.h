@@ -21,6 +21,15 @@ struct CamDev {
     double pad[3];
 };
 
+// Window moments of one view at one pixel, 12 bytes: w = 1/sqrt(n S_bb - S_b^2)
+// (binary64, 0 for a constant window) and S_b.  S_bb is implied:
+// n S_bb - S_b^2 = rint(1/w^2) exactly (db < 2^31, w within 3 ulp).
+struct __attribute__((packed, aligned(4))) MomEntry {
+    double w;
+    uint32_t sb;
+};
+static_assert(sizeof(MomEntry) == 12, "12-byte moments entries");
+
 // Device-resident scene: the gray stack in quad-interleaved pixel-major
 // layout  stack[y][k][v][4] = gray_v(y, 4k..4k+3)  (k = quad index), so that
 // one window row of every view is one contiguous run, and one dword holds
@@ -36,11 +45,11 @@ struct SceneDev {
     // view's window rows are read with scalar (SMEM) loads
     const uint8_t* gv;
     int Wp;
-    // per-view window moments mom[wid][(y*W + x)*V + v] = (S_b, S_bb) of the
-    // (2wid+1)^2 window centred at (x, y) (0 where the window is invalid);
-    // built once per scene and wid -- the np.mean/np.std ingredients of
-    // ctNcc, which do not depend on the reference view
-    const uint2* mom[MVS_MAX_WID + 1];
+    // per-view window moments mom[wid][(y*W + x)*V + v] of the (2wid+1)^2
+    // window centred at (x, y) (zero where the window is invalid); built once
+    // per scene and wid -- the np.mean/np.std ingredients of ctNcc, which do
+    // not depend on the reference view
+    const struct MomEntry* mom[MVS_MAX_WID + 1];
 };
 
 // Inputs/outputs of one scoring batch (device pointers).
@@ -117,7 +126,7 @@ int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_
                      hipEvent_t ev0, hipEvent_t ev1);
 int mvs_launch_build_gv(const uint8_t* d_stack, uint8_t* d_gv, int V, int H, int W, int Wq, int Wp,
                         hipStream_t s);
-int mvs_launch_build_moments(const SceneDev* sc, int wid, uint2* d_mom, hipStream_t s);
+int mvs_launch_build_moments(const SceneDev* sc, int wid, MomEntry* d_mom, hipStream_t s);
 // Tile geometry of the tiled scorers for a W x H image (so the host can size
 // scratch): mfma != 0 -> the MFMA scorer's 16x16 tiles, else 16x8.
 void mvs_tiled_geometry(int W, int H, int mfma, int* tw, int* th, int* ntx, int* nty);

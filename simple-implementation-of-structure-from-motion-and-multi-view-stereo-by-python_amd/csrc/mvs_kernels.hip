@@ -61,6 +61,20 @@ DEV uint8_t stack_px(const SceneDev& sc, int view, int y, int x) {
     return sc.stack[(int64_t)y * sc.row_bytes + (int64_t)(x >> 2) * sc.V * 4 + view * 4 + (x & 3)];
 }
 
+// One 12-byte moments entry as three dword loads (4-byte aligned).
+DEV MomEntry load_mom(const MomEntry* m, int64_t idx) {
+    const uint32_t* p = (const uint32_t*)m + 3 * idx;
+    MomEntry e;
+    e.w = __longlong_as_double(((unsigned long long)p[1] << 32) | p[0]);
+    e.sb = p[2];
+    return e;
+}
+
+// n S_bb - S_b^2 of an entry, exactly (see MomEntry)
+DEV int32_t mom_db(const MomEntry& m) {
+    return m.w > 0.0 ? (int32_t)rint(1.0 / (m.w * m.w)) : 0;
+}
+
 // numpy pairwise sum of (x_i - mean)^2 for n <= 128 (8 accumulators).
 template <class F>
 DEV double pairwise_sq(F&& xi, int n) {
@@ -115,20 +129,27 @@ DEV double dpp_f64(double x) {
     return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// row_bcast:15 / row_bcast:31 (GFX9 DPP): rows in ROWMASK receive the last lane
+// of the row before / of row 1; the other rows get 0
+template <int CTRL, int ROWMASK>
+DEV double dpp_bcast_f64(double x) {
+    const unsigned long long u = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROWMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROWMASK, 0xf, false);
+    return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 DEV double wave_sum_dpp(double x) {
     x += dpp_f64<0xB1>(x);    // quad_perm [1,0,3,2]
     x += dpp_f64<0x4E>(x);    // quad_perm [2,3,0,1]
     x += dpp_f64<0x141>(x);   // row_half_mirror
     x += dpp_f64<0x140>(x);   // row_mirror: every lane holds its row's sum
+    x += dpp_bcast_f64<0x142, 0xa>(x);   // rows 1, 3 += rows 0, 2
+    x += dpp_bcast_f64<0x143, 0xc>(x);   // rows 2, 3 += rows 0+1: lane 63 holds the total
     const unsigned long long u = __double_as_longlong(x);
-    double r[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, 16 * k);
-        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 16 * k);
-        r[k] = __longlong_as_double(((unsigned long long)hi << 32) | lo);
-    }
-    return (r[0] + r[1]) + (r[2] + r[3]);
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, 63);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
 DEV double wave_sum(double x) {
@@ -497,7 +518,7 @@ struct TileGeom {
 // and rank it inside its tile.  Ranks come from an LDS histogram per block
 // (one global atomic per non-empty (block, tile) pair), not from a global
 // atomic per candidate.
-constexpr int kBinBlock = 1024, kBinPer = 8;
+constexpr int kBinBlock = 1024, kBinPer = 4;
 
 __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t, int wid) {
@@ -692,10 +713,11 @@ __global__ void k_build_gv(const uint8_t* __restrict__ stack, uint8_t* __restric
     }
 }
 
-// (S_b, S_bb) of every view's window at every valid centre; one thread per
-// (pixel, view), rows summed from the aligned words of the stack.
+// (S_b, S_bb, 1/sqrt(n S_bb - S_b^2)) of every view's window at every valid
+// centre; one thread per (pixel, view), rows summed from the aligned words of
+// the stack.
 template <int WID>
-__global__ void k_moments(const SceneDev sc, uint2* __restrict__ mom) {
+__global__ void k_moments(const SceneDev sc, MomEntry* __restrict__ mom) {
     constexpr int NB = 2 * WID + 1, NW = (NB + 3) / 4;
     constexpr uint32_t LASTMASK = (NB % 4 == 0) ? 0xffffffffu : ((1u << (8 * (NB % 4))) - 1u);
     const int64_t total = (int64_t)sc.H * sc.W * sc.V;
@@ -704,7 +726,7 @@ __global__ void k_moments(const SceneDev sc, uint2* __restrict__ mom) {
         const int v = (int)(id % sc.V);
         const int64_t p = id / sc.V;
         const int x = (int)(p % sc.W), y = (int)(p / sc.W);
-        uint2 out = make_uint2(0, 0);
+        MomEntry out{0.0, 0u};
         if (y - WID >= 0 && y + WID + 1 < sc.H && x - WID > 0 && x + WID + 1 < sc.W) {
             const int q0 = x - WID, k0 = q0 >> 2, o = q0 & 3;
             uint32_t sb = 0, sbb = 0;
@@ -722,9 +744,15 @@ __global__ void k_moments(const SceneDev sc, uint2* __restrict__ mom) {
                     sbb = __builtin_amdgcn_udot4(w, w, sbb, false);
                 }
             }
-            out = make_uint2(sb, sbb);
+            const int64_t db = (int64_t)(NB * NB) * sbb - (int64_t)sb * sb;
+            out.sb = sb;
+            out.w = db > 0 ? 1.0 / sqrt((double)db) : 0.0;
         }
-        mom[id] = out;
+        uint32_t* o = (uint32_t*)mom + 3 * id;
+        const unsigned long long wb = __double_as_longlong(out.w);
+        o[0] = (uint32_t)wb;
+        o[1] = (uint32_t)(wb >> 32);
+        o[2] = out.sb;
     }
 }
 
@@ -876,7 +904,7 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
     // wave index as an SGPR: the candidate loop, its SMEM loads and the
     // alignment switch below are then scalar control flow
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint2* __restrict__ mom = sc.mom[WID];
+    const MomEntry* __restrict__ mom = sc.mom[WID];
     // output staging behind the region image (chunk <= kChunk candidates)
     uint64_t* o_mask = (uint64_t*)(lds + G::ROWS * RS);
     double* o_avg = (double*)(o_mask + t.chunk);
@@ -942,34 +970,42 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
             return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
         };
         int2 cur = cb + wave < ce ? sload(t.sorted + cb + wave) : make_int2(0, 0);
-        uint2 mb_cur = make_uint2(0, 0);
+        MomEntry mb_cur{0.0, 0u};
         if (cb + wave < ce) {
             const int pk = cur.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
-            if (lane < V) mb_cur = mom[(r * sc.W + q) * V + lane];
+            if (lane < V) mb_cur = load_mom(mom, (r * sc.W + q) * V + lane);
         }
         for (int j = cb + wave; j < ce; j += kT3Waves) {
             const int2 nxt = j + kT3Waves < ce ? sload(t.sorted + j + kT3Waves) : make_int2(0, 0);
-            uint2 mb_nxt = make_uint2(0, 0);
+            MomEntry mb_nxt{0.0, 0u};
             if (j + kT3Waves < ce) {
                 const int pk = nxt.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
-                if (lane < V) mb_nxt = mom[(r * sc.W + q) * V + lane];
+                if (lane < V) mb_nxt = load_mom(mom, (r * sc.W + q) * V + lane);
             }
             const int pk = cur.y;
             const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
             const int q0 = q - WID, o = q0 & 3;
             const int k0 = (q0 >> 2) - kq0;
-            const uint2 mb = mb_cur;
-            const uint2 ma = make_uint2(__builtin_amdgcn_readlane(mb.x, R), __builtin_amdgcn_readlane(mb.y, R));
+            const MomEntry mb = mb_cur;
+            // the reference view's moments: lane R's entry
+            const uint32_t ma_sb = __builtin_amdgcn_readlane(mb.sb, R);
+            const uint2 wa2 = make_uint2(__builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mb.w), R),
+                                         __builtin_amdgcn_readlane((uint32_t)((uint64_t)__double_as_longlong(mb.w) >> 32), R));
+            const double wa = __longlong_as_double(((uint64_t)wa2.y << 32) | wa2.x);
             const uint32_t* basep = lds + (r - WID - y0) * RS + k0 * QS + lane;
             // the reference view's quads: same LDS address in every lane (broadcast)
             const uint32_t* refl = basep - lane + R;
-            uint32_t Sab;
+            uint32_t Sab = 0;
             if constexpr (REFSRC == 0) {
-                switch (o) {   // wave-uniform: window byte offset inside the first quad
-                    case 0: Sab = sab_rows<WID, 0, RS, QS>(basep, refl); break;
-                    case 1: Sab = sab_rows<WID, 1, RS, QS>(basep, refl); break;
-                    case 2: Sab = sab_rows<WID, 2, RS, QS>(basep, refl); break;
-                    default: Sab = sab_rows<WID, 3, RS, QS>(basep, refl); break;
+                // lanes past the last view issue no LDS reads: at V = 48 that is a
+                // quarter of the LDS traffic, and LDS bandwidth is a bound here
+                if (lane < V) {
+                    switch (o) {   // wave-uniform: window byte offset inside the first quad
+                        case 0: Sab = sab_rows<WID, 0, RS, QS>(basep, refl); break;
+                        case 1: Sab = sab_rows<WID, 1, RS, QS>(basep, refl); break;
+                        case 2: Sab = sab_rows<WID, 2, RS, QS>(basep, refl); break;
+                        default: Sab = sab_rows<WID, 3, RS, QS>(basep, refl); break;
+                    }
                 }
             } else {
                 cgu32* refg = (cgu32*)(sc.gv + ((int64_t)R * sc.H + (r - WID)) * sc.Wp + 4 * (q0 >> 2));
@@ -981,47 +1017,41 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
                     default: Sab = sab_rows_smem<WID, 3, RS, QS>(basep, refg, pitch); break;
                 }
             }
-            // |num|, da, db < 2^31 for windows up to 11x11 (sums < 2^24): 24-bit
-            // multiplies, exact
+            // num = n S_ab - S_a S_b (|num| < 2^31 for windows up to 11x11: 24-bit
+            // multiplies, exact).  With w = 1/sqrt(n S_bb - S_b^2) per (pixel, view)
+            // from the moments table, ctNcc * (n-1) = n num w_a w_b; it is
+            // compared with thr (n-1).  The three roundings leave < 2e-15 relative
+            // error, so a relative band of 1e-8 around the threshold (far wider
+            // than the reference's own rounding) goes to k_score_fix, which
+            // decides those lanes with the numpy-order ctNcc.
             static_assert(NPX <= 121, "24-bit moment products need NB <= 11");
-            const int32_t da = (int32_t)(__umul24(NPX, ma.y) - __umul24(ma.x, ma.x));
-            const int32_t db = (int32_t)(__umul24(NPX, mb.y) - __umul24(mb.x, mb.x));
-            const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma.x, mb.x));
-            const bool live = lane < V && lane != R && da > 0 && db > 0;
+            const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma_sb, mb.sb));
+            const bool live = lane < V && lane != R && mb.w > 0.0 && wa > 0.0;
             bool pass = false, guard = false;
             double ncc = 0.0;
             if (live) {
                 if (a.thr >= 0.01) {
-                    // ncc > thr  <=>  L > 0 and L^2 > thr^2 (n-1)^2 da db, L = n*num
-                    // (exact in binary64); a relative band of 1e-8 around equality
-                    // goes to k_score_fix (numpy-order ctNcc)
-                    const double L = (double)num * (double)NPX;
-                    if (L > 0.0) {
-                        const double tk = a.thr * (double)(NPX - 1);
-                        const double rhs = (tk * tk) * ((double)da * (double)db);
-                        const double diff = L * L - rhs;
-                        guard = fabs(diff) <= 1e-8 * rhs;
-                        pass = diff > 0.0;
-                        if (pass && a.avg) {
-                            const double D = (double)da * (double)db;
-                            double y = __builtin_amdgcn_rsq(D);
-                            y = y * (1.5 - 0.5 * D * y * y);
-                            y = y * (1.5 - 0.5 * D * y * y);
-                            ncc = L * y * (1.0 / (double)(NPX - 1));
-                        }
-                    }
+                    const double tk = a.thr * (double)(NPX - 1);
+                    const double z = ((double)num * ((double)NPX * wa)) * mb.w;   // ncc (n-1)
+                    guard = fabs(z - tk) <= 1e-8 * tk;
+                    pass = z > tk;
+                    ncc = z;
                 } else {
+                    const int32_t db = mom_db(mb);
+                    const int32_t da = __builtin_amdgcn_readlane(db, R);
                     ncc = ((double)num * (double)NPX) /
                           ((double)(NPX - 1) * sqrt((double)da * (double)db));
                     guard = fabs(ncc - a.thr) <= kGuard;
                     pass = ncc > a.thr;
+                    ncc *= (double)(NPX - 1);
                 }
             }
             if (__ballot(guard) != 0 && lane == 0) t.fix_list[atomicAdd(t.fix_count, 1)] = cur.x;
             const uint64_t m = __ballot(pass);
             const int cnt = __popcll(m);
             double avgv = 0.0;
-            if (a.avg && cnt) avgv = wave_sum_dpp(pass ? ncc : 0.0) * c_recip.r[cnt];
+            if (a.avg && cnt)
+                avgv = wave_sum_dpp(pass ? ncc : 0.0) * (c_recip.r[cnt] * (1.0 / (double)(NPX - 1)));
             const int slot = j - cb;
             if (lane == 0) {
                 o_mask[slot] = m;
@@ -1113,7 +1143,7 @@ __global__ __launch_bounds__(kMThreads, 2) void k_score_mfma(const SceneDev sc, 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n_items = t.item_off[t.ntiles];
     const int nkey = V * kMTH;
-    const uint2* __restrict__ mom = sc.mom[WID];
+    const MomEntry* __restrict__ mom = sc.mom[WID];
     const int lx = lane & 15, lh = lane >> 4;
     // A-fragment band mask of this lane: output x = lx, region columns 16 lh + b
     uint32_t bm[4];
@@ -1234,7 +1264,8 @@ __global__ __launch_bounds__(kMThreads, 2) void k_score_mfma(const SceneDev sc, 
                     if (pb + c < pe && lane < V) {
                         const int pk = cs[pb + c].y;
                         const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
-                        mbs[c] = mom[(r * sc.W + q) * V + lane];
+                        { const MomEntry me = load_mom(mom, (r * sc.W + q) * V + lane);
+                          mbs[c] = make_uint2(me.sb, (uint32_t)(((int64_t)mom_db(me) + (int64_t)me.sb * me.sb) / NPX)); }
                     }
                 }
                 // MFMA rows: ring of prefixes C_y over the region rows
@@ -1348,6 +1379,310 @@ __global__ __launch_bounds__(kMThreads, 2) void k_score_mfma(const SceneDev sc, 
             a.mask[i] = o_mask[k];
             a.count[i] = o_cnt[k];
             if (a.avg) a.avg[i] = o_avg[k];
+        }
+        __syncthreads();
+        STAMP(3);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// MFMA scorer, v2 (variant 9): same 16x8 tiles and work items as
+// k_score_tiled3; per (tile, reference view R) the S_ab sums of every output
+// pixel against every view come from v_mfma_i32_16x16x32_i8 chains, one
+// 16-view slice at a time:  C_y = A_y . B_y + C_{y-1}  over the 8 + 2 WID
+// region rows, A_y(x, k) = g_R(y, k) - 128 masked to the window columns of
+// output x (k = 32 region columns = the MFMA's K), B_y(k, v) = g_v(y, k) - 128;
+// S(output row j) = C_{j+2WID} - C_{j-1}.  Only the S values of the item's
+// candidates are kept (per-wave LDS buffer); the decision epilogue is
+// k_score_tiled3's.  Operand bytes per MFMA: 512 (B) + 512 (A, LDS
+// broadcast), against ~15 KB of LDS reads per candidate in tiled3.
+// ---------------------------------------------------------------------------
+typedef long v1l;
+constexpr int kM2Threads = 256, kM2Waves = kM2Threads / 64;
+constexpr int kM2NB = 16;                    // candidates per R pass
+
+template <int WID, int NT>
+struct Mfma2Geom {
+    static constexpr int NB = 2 * WID + 1;
+    static constexpr int NR = kTH + 2 * WID;        // region rows
+    static constexpr int VS = NR * 32 + 8;          // bytes per view: an odd number of 8-B units
+    static constexpr int NV = NT * 16;
+    static constexpr int NKEY = 64 * kTH;           // (R, output row), V <= 64
+    static constexpr int OFF0 = (4 - WID % 4) % 4;  // region column of output x's window = x + OFF0
+    static_assert(kTW + OFF0 + 2 * WID <= 32, "window must fit the 32 region columns");
+    static constexpr int O_REG = 0;
+    static constexpr int O_CS = (NV * VS + 15) / 16 * 16;              // int2[kM2Threads]
+    static constexpr int O_HS = O_CS + 8 * kM2Threads;                  // int[NKEY + 4]
+    static constexpr int O_CUR = O_HS + 4 * (NKEY + 4);                // int[NKEY]
+    static constexpr int O_SB = O_CUR + 4 * NKEY;                      // int[waves][kM2NB][NV]
+    static constexpr int O_OM = O_SB + 4 * kM2Waves * kM2NB * NV;      // u64[kM2Threads]
+    static constexpr int O_OA = O_OM + 8 * kM2Threads;                 // double[kM2Threads]
+    static constexpr int O_OC = O_OA + 8 * kM2Threads;                 // int[kM2Threads]
+    static constexpr int O_WT = O_OC + 4 * kM2Threads;                 // int[waves]
+    static constexpr int BYTES = O_WT + 4 * kM2Waves;
+};
+
+template <int WID, int NT>
+__global__ __launch_bounds__(kM2Threads, 3) void k_score_mfma2(const SceneDev sc, const ScoreArgs a,
+                                                               const TiledArgs t) {
+    using G = Mfma2Geom<WID, NT>;
+    constexpr int NB = G::NB, NPX = NB * NB, NR = G::NR, VS = G::VS, NV = G::NV;
+    constexpr int RING = NB + 1;              // prefixes C_{y-NB} .. C_y
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint8_t* reg = smem + G::O_REG;
+    int2* cs = (int2*)(smem + G::O_CS);
+    int* hs = (int*)(smem + G::O_HS);
+    int* cur = (int*)(smem + G::O_CUR);
+    int* sbuf = (int*)(smem + G::O_SB);
+    uint64_t* o_mask = (uint64_t*)(smem + G::O_OM);
+    double* o_avg = (double*)(smem + G::O_OA);
+    int32_t* o_cnt = (int32_t*)(smem + G::O_OC);
+    int* wt = (int*)(smem + G::O_WT);
+    __shared__ int s_item;
+
+    const int V = sc.V;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n_items = t.item_off[t.ntiles];
+    const int nkey = V * kTH;
+    const MomEntry* __restrict__ mom = sc.mom[WID];
+    const int lx = lane & 15, lh = lane >> 4;
+    // A-operand band mask of this lane: output x = lx, region columns 8 lh + b
+    uint32_t bm[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int col = 8 * lh + 4 * d + b;
+            if (col >= lx + G::OFF0 && col <= lx + G::OFF0 + 2 * WID) m |= 0xffu << (8 * b);
+        }
+        bm[d] = m;
+    }
+    int* my_sb = sbuf + wave * kM2NB * NV;
+#ifdef MVS_STAMPS
+    unsigned long long st_prev = 0;
+#endif
+
+    for (;;) {
+        if (tid == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
+        __syncthreads();
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item >= n_items) break;
+        STAMP(0);
+        int lo = 0, hi = t.ntiles;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t.item_off[mid] <= item) lo = mid; else hi = mid;
+        }
+        const int tile = lo;
+        const int cb = t.tile_off[tile] + (item - t.item_off[tile]) * t.chunk;
+        const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
+        const int nc = ce - cb;                 // <= kM2Threads
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int x0 = tx * kTW, yo0 = ty * kTH;
+        const int y0 = yo0 - WID;
+        const int kq0 = (x0 - WID) >> 2;        // floor
+        // ---- stage the region (NR rows x 8 quads x all views) as g ^ 0x80 ----
+        {
+            const int cpq = V >> 2, cpr = 8 * cpq, total = NR * cpr;
+            for (int base = 0; base < total; base += 4 * kM2Threads) {
+                uint4 buf[4];
+                int dst[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = base + u * kM2Threads + tid;
+                    dst[u] = -1;
+                    buf[u] = make_uint4(0, 0, 0, 0);
+                    if (k < total) {
+                        const int ry = k / cpr, rem = k - ry * cpr;
+                        const int kq = rem / cpq, vq = rem - kq * cpq;
+                        const int y = y0 + ry, gq = kq0 + kq;
+                        if (y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                            buf[u] = *(const uint4*)(sc.stack + (int64_t)y * sc.row_bytes +
+                                                      (int64_t)gq * V * 4 + vq * 16);
+                        dst[u] = (4 * vq) * VS + ry * 32 + kq * 4;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (dst[u] >= 0) {
+                        uint8_t* d = smem + G::O_REG + dst[u];
+                        *(uint32_t*)(d) = buf[u].x ^ 0x80808080u;
+                        *(uint32_t*)(d + VS) = buf[u].y ^ 0x80808080u;
+                        *(uint32_t*)(d + 2 * VS) = buf[u].z ^ 0x80808080u;
+                        *(uint32_t*)(d + 3 * VS) = buf[u].w ^ 0x80808080u;
+                    }
+            }
+        }
+        // ---- the item's candidates (one per thread), counting-sorted by (R, row) ----
+        for (int k = tid; k < nkey; k += kM2Threads) cur[k] = 0;
+        __syncthreads();
+        int2 e = make_int2(0, 0);
+        int key = -1;
+        if (tid < nc) {
+            e = t.sorted[cb + tid];
+            const int r = (e.y >> 11) & 0x7ff, R = (e.y >> 22) & 0x3ff;
+            key = R * kTH + (r - yo0);
+            atomicAdd(&cur[key], 1);
+        }
+        __syncthreads();
+        {   // exclusive scan of cur[0 .. nkey) into hs (two keys per thread)
+            const int b = 2 * tid;
+            const int c0 = b < nkey ? cur[b] : 0, c1 = b + 1 < nkey ? cur[b + 1] : 0;
+            int sum = c0 + c1;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int u = __shfl_up(sum, off, 64);
+                if (lane >= off) sum += u;
+            }
+            if (lane == 63) wt[wave] = sum;
+            __syncthreads();
+            int before = 0;
+            for (int w = 0; w < wave; ++w) before += wt[w];
+            const int excl = before + sum - (c0 + c1);
+            if (b < nkey) { hs[b] = excl; cur[b] = excl; }
+            if (b + 1 < nkey) { hs[b + 1] = excl + c0; cur[b + 1] = excl + c0; }
+            if (tid == kM2Threads - 1) hs[nkey] = before + sum;
+        }
+        __syncthreads();
+        if (key >= 0) cs[atomicAdd(&cur[key], 1)] = e;
+        __syncthreads();
+        STAMP(1);
+        // ---- one reference view per wave at a time ----
+        for (int R = wave; R < V; R += kM2Waves) {
+            const int gb = __builtin_amdgcn_readfirstlane(hs[R * kTH]);
+            const int ge = __builtin_amdgcn_readfirstlane(hs[(R + 1) * kTH]);
+            for (int pb = gb; pb < ge; pb += kM2NB) {
+                const int np = min(kM2NB, ge - pb);
+                STAMP_T(tp0);
+                // the pass's candidates: lane c holds candidate pb + c's packed
+                // (q, r, R); their moments are fetched now and used after the rows
+                const int pkv = lane < np ? cs[pb + lane].y : 0;
+                // moments of candidate c (this lane's view), two candidates ahead
+                auto mom_of = [&](int c) -> uint2 {
+                    uint2 m = make_uint2(0, 0);
+                    if (c < np) {
+                        const int pk = __builtin_amdgcn_readlane(pkv, c);
+                        if (lane < V) { const MomEntry me = load_mom(mom, (((pk >> 11) & 0x7ff) * sc.W + (pk & 0x7ff)) * V + lane);
+                                        m = make_uint2(me.sb, (uint32_t)(((int64_t)mom_db(me) + (int64_t)me.sb * me.sb) / NPX)); }
+                    }
+                    return m;
+                };
+                uint2 mb0 = mom_of(0), mb1 = mom_of(1);
+                // masked A operands of all region rows (LDS broadcast reads)
+                v1l Af[NR];
+                {
+                    const uint8_t* ra = reg + R * VS + 8 * lh;
+#pragma unroll
+                    for (int y = 0; y < NR; ++y) {
+                        const uint2 w = *(const uint2*)(ra + y * 32);
+                        Af[y] = (v1l)((uint64_t)(w.x & bm[0]) | ((uint64_t)(w.y & bm[1]) << 32));
+                    }
+                }
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const uint8_t* rb = reg + (16 * nt + lx) * VS + 8 * lh;
+                    v1l Bf[NR];
+#pragma unroll
+                    for (int y = 0; y < NR; ++y) {
+                        const uint2 w = *(const uint2*)(rb + y * 32);
+                        Bf[y] = (v1l)((uint64_t)w.x | ((uint64_t)w.y << 32));
+                    }
+                    v4i C[RING];
+                    int kk = 0;   // next candidate of the pass (sorted by output row)
+#pragma unroll
+                    for (int y = 0; y < NR; ++y) {
+                        const v4i zero = {0, 0, 0, 0};
+                        C[y % RING] = __builtin_amdgcn_mfma_i32_16x16x32_i8(
+                            Af[y], Bf[y], y == 0 ? zero : C[(y + RING - 1) % RING], 0, 0, 0);
+                        if (y >= 2 * WID) {
+                            const int j = y - 2 * WID;   // output row
+                            while (kk < np) {
+                                const int pk = __builtin_amdgcn_readlane(pkv, kk);
+                                if (((pk >> 11) & 0x7ff) - yo0 != j) break;
+                                const int x = (pk & 0x7ff) - x0;
+                                const int xi = x & 3;
+                                // S_j at (x, v) = C_{j+2WID} - C_{j-1}; C_{j-1} is slot (y+1) % RING
+                                const v4i Cy = C[y % RING];
+                                const v4i Cp = j == 0 ? zero : C[(y + 1) % RING];
+                                const int val = xi == 0 ? Cy[0] - Cp[0] : xi == 1 ? Cy[1] - Cp[1]
+                                              : xi == 2 ? Cy[2] - Cp[2] : Cy[3] - Cp[3];
+                                if (lh == (x >> 2)) my_sb[kk * NV + 16 * nt + lx] = val;
+                                ++kk;
+                            }
+                        }
+                    }
+                }
+                STAMP_T(tp1);
+                STAMP_ADD(4, tp0, tp1);
+                // decision epilogue: one lane per view, as k_score_tiled3
+                for (int c = 0; c < np; ++c) {
+                    const int k = pb + c;
+                    const int ci = __builtin_amdgcn_readfirstlane(cs[k].x);
+                    const uint2 mb = mb0;
+                    mb0 = mb1;
+                    mb1 = mom_of(c + 2);
+                    const uint2 ma = make_uint2(__builtin_amdgcn_readlane(mb.x, R),
+                                                __builtin_amdgcn_readlane(mb.y, R));
+                    const int sab_s = lane < NV ? my_sb[c * NV + lane] : 0;
+                    const uint32_t Sab = (uint32_t)(sab_s + 128 * (int)(ma.x + mb.x) - 16384 * NPX);
+                    const int32_t da = (int32_t)(__umul24(NPX, ma.y) - __umul24(ma.x, ma.x));
+                    const int32_t db = (int32_t)(__umul24(NPX, mb.y) - __umul24(mb.x, mb.x));
+                    const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma.x, mb.x));
+                    const bool live = lane < V && lane != R && da > 0 && db > 0;
+                    bool pass = false, guard = false;
+                    double ncc = 0.0;
+                    if (live) {
+                        if (a.thr >= 0.01) {
+                            const double L = (double)num * (double)NPX;
+                            if (L > 0.0) {
+                                const double tk = a.thr * (double)(NPX - 1);
+                                const double rhs = (tk * tk) * ((double)da * (double)db);
+                                const double diff = L * L - rhs;
+                                guard = fabs(diff) <= 1e-8 * rhs;
+                                pass = diff > 0.0;
+                                if (pass && a.avg) {
+                                    const double D = (double)da * (double)db;
+                                    double yv = __builtin_amdgcn_rsq(D);
+                                    yv = yv * (1.5 - 0.5 * D * yv * yv);
+                                    yv = yv * (1.5 - 0.5 * D * yv * yv);
+                                    ncc = L * yv * (1.0 / (double)(NPX - 1));
+                                }
+                            }
+                        } else {
+                            ncc = ((double)num * (double)NPX) /
+                                  ((double)(NPX - 1) * sqrt((double)da * (double)db));
+                            guard = fabs(ncc - a.thr) <= kGuard;
+                            pass = ncc > a.thr;
+                        }
+                    }
+                    if (__ballot(guard) != 0 && lane == 0)
+                        t.fix_list[atomicAdd(t.fix_count, 1)] = ci;
+                    const uint64_t m = __ballot(pass);
+                    const int cnt = __popcll(m);
+                    double avgv = 0.0;
+                    if (a.avg && cnt) avgv = wave_sum_dpp(pass ? ncc : 0.0) * c_recip.r[cnt];
+                    if (lane == 0) {
+                        o_mask[k] = m;
+                        o_avg[k] = avgv;
+                        o_cnt[k] = cnt;
+                    }
+                }
+                const int pe = pb + np;
+                STAMP_T(tp2);
+                STAMP_ADD(5, tp1, tp2);
+                STAMP_ADD(6, 0, (unsigned long long)(pe - pb));
+            }
+        }
+        __syncthreads();
+        STAMP(2);
+        if (tid < nc) {
+            const int i = cs[tid].x;
+            a.mask[i] = o_mask[tid];
+            a.count[i] = o_cnt[tid];
+            if (a.avg) a.avg[i] = o_avg[tid];
         }
         __syncthreads();
         STAMP(3);
@@ -1532,6 +1867,12 @@ void launch_mfma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hip
     k_score_mfma<WID, NT><<<dim3(kTiledBlocks / 2), dim3(kMThreads), lds, s>>>(*sc, *a, *t);
 }
 
+template <int WID, int NT>
+void launch_mfma2(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s) {
+    constexpr size_t lds = Mfma2Geom<WID, NT>::BYTES;
+    k_score_mfma2<WID, NT><<<dim3(kTiledBlocks), dim3(kM2Threads), lds, s>>>(*sc, *a, *t);
+}
+
 template <int WID>
 int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int variant,
                          hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
@@ -1546,6 +1887,22 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
     const size_t lds = (size_t)G::ROWS * G::NQ * 64 * 4;
+    if (variant == 9) {
+        if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kM2Threads || t->th != kTH ||
+            t->tw != kTW)
+            return -3;
+        {
+            TimedLaunch tl(s, ev0, ev1);
+            switch ((sc->V + 15) / 16) {
+                case 1: launch_mfma2<WID, 1>(sc, a, t, s); break;
+                case 2: launch_mfma2<WID, 2>(sc, a, t, s); break;
+                case 3: launch_mfma2<WID, 3>(sc, a, t, s); break;
+                default: launch_mfma2<WID, 4>(sc, a, t, s); break;
+            }
+        }
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(64), dim3(256), 0, s, *sc, *a, *t);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (variant == 6) {
         if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kMChunk || t->th != kMTH ||
             t->tw != kMTW)
@@ -1630,7 +1987,7 @@ extern "C" int mvs_launch_build_gv(const uint8_t* d_stack, uint8_t* d_gv, int V,
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mvs_launch_build_moments(const SceneDev* sc, int wid, uint2* d_mom, hipStream_t s) {
+extern "C" int mvs_launch_build_moments(const SceneDev* sc, int wid, MomEntry* d_mom, hipStream_t s) {
     switch (wid) {
         case 1: hipLaunchKernelGGL(k_moments<1>, dim3(8192), dim3(256), 0, s, *sc, d_mom); break;
         case 2: hipLaunchKernelGGL(k_moments<2>, dim3(8192), dim3(256), 0, s, *sc, d_mom); break;
