@@ -12,3 +12,4 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_
   rc=$?; echo "pass $i ($grp) rc=$rc"
   [ $rc -ne 0 ] && { tail -5 gpurun_out/pmc_${TAG}_p$i.log; exit $rc; }
 done
+exit 0
