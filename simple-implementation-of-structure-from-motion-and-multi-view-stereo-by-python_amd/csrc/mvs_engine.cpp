@@ -281,7 +281,8 @@ struct mvs_ctx {
     DevBuf<int32_t> s_ref, s_count;
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
-    DevBuf<int32_t> t_tiles, t_cand;
+    DevBuf<int32_t> t_tiles, t_cand, t_pcnt;
+    DevBuf<double> t_psum;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
     int variant = 0;       // tiled-kernel variant (env MVS_VARIANT), see mvs_kernels.hip
     int chunk3 = 256;      // candidates per work item of the v3 tiled kernel (env MVS_TILE_CHUNK)
@@ -377,10 +378,15 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
     a.count = d_count;
     a.avg = d_avg;
     a.exact_hits = ctx->d_exact.p;
-    const bool tiled = ctx->V <= 64 && (ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048));
+    // tiled scorers: k_score_tiled3 (V <= 64) and the view-group k_score_tiledg
+    // (64 < V <= 256, V a multiple of 4); the direct k_score takes the rest and
+    // small batches
+    const bool grouped = ctx->V > 64;
+    const bool tiled_ok = !grouped || ((ctx->V & 3) == 0 && ctx->V <= 256);
+    const bool tiled = tiled_ok && (ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048));
     // the MFMA scorer stages 16-B groups of 4 views: other view counts take the 16x8 tiled path
-    const int variant = ((ctx->variant == 6 || ctx->variant == 9) && (ctx->V & 3) != 0) ? 0 : ctx->variant;
-    if (tiled && (variant == 0 || variant >= 4) && (ctx->V & 3) == 0 &&
+    const int variant = grouped || ((ctx->variant == 6 || ctx->variant == 9) && (ctx->V & 3) != 0) ? 0 : ctx->variant;
+    if (tiled && (grouped || variant == 0 || variant >= 4) && (ctx->V & 3) == 0 &&
         !ctx->sc.mom[wid]) {
         // scene moments for this window size: built once, reused by every batch
         ctx->d_mom[wid].alloc((size_t)ctx->H * ctx->W * ctx->V);
@@ -394,9 +400,17 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         mvs_tiled_geometry(ctx->W, ctx->H, mfma ? 1 : 0, &t.tw, &t.th, &t.ntx, &t.nty);
         const int ntiles = t.ntx * t.nty;
         ctx->t_tiles.ensure((size_t)3 * (ntiles + 2));
-        ctx->t_cand.ensure((size_t)6 * n);
+        const int groups = grouped ? (ctx->V + 63) / 64 : 1;
+        ctx->t_cand.ensure((size_t)(5 + groups) * n);   // fix_list: one entry per (candidate, group)
         t.ntiles = ntiles;
-        t.chunk = mfma ? 1024 : variant == 9 ? 256 : (variant == 0 || variant >= 4) ? ctx->chunk3 : 512;
+        t.chunk = grouped ? ctx->chunk3 : mfma ? 1024 : variant == 9 ? 256 : (variant == 0 || variant >= 4) ? ctx->chunk3 : 512;
+        t.groups = groups;
+        if (grouped) {
+            ctx->t_pcnt.ensure((size_t)groups * n);
+            ctx->t_psum.ensure((size_t)groups * n);
+            t.part_cnt = ctx->t_pcnt.p;
+            t.part_sum = ctx->t_psum.p;
+        }
         t.tile_count = ctx->t_tiles.p;
         t.tile_off = ctx->t_tiles.p + (ntiles + 2);
         t.item_off = ctx->t_tiles.p + 2 * (ntiles + 2);

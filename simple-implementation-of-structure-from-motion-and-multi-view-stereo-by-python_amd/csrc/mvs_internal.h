@@ -84,6 +84,12 @@ struct TiledArgs {
     int2* sorted;
     int32_t* fix_list;
     int32_t* fix_count;
+    // view groups (V > 64, k_score_tiledg): work item = (tile chunk, group of
+    // 64 views); per (candidate, group) partial count and sum of passing
+    // ncc*(n-1), reduced by k_group_finalize.  groups = 1 otherwise.
+    int groups;
+    int32_t* part_cnt;         // n*groups
+    double* part_sum;          // n*groups
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).

@@ -782,7 +782,9 @@ struct QuadMasks {
 
 using lds_u32 = __attribute__((address_space(3))) const uint32_t;
 
-template <int WID, int O, int RS, int QS>
+// The reference quads sit at the same strides (RRS, RQS) = (RS, QS) when they
+// come from the region image, or in a per-wave [row][4] slot (RRS 4, RQS 1).
+template <int WID, int O, int RS, int QS, int RRS = RS, int RQS = QS>
 DEV uint32_t sab_rows(const uint32_t* own_g, const uint32_t* ref_g) {
     using M = QuadMasks<WID, O>;
     constexpr int NB = 2 * WID + 1;
@@ -793,13 +795,13 @@ DEV uint32_t sab_rows(const uint32_t* own_g, const uint32_t* ref_g) {
         // multiple of 64 when RS = 8*48), so each column's 11 rows pair up
         // into ds_read2st64_b32 off that base with no further address math
         lds_u32* o = (lds_u32*)own_g + jj * QS;
-        lds_u32* r = (lds_u32*)ref_g + jj * QS;
+        lds_u32* r = (lds_u32*)ref_g + jj * RQS;
         asm volatile("" : "+v"(o));
         asm volatile("" : "+v"(r));
 #pragma unroll
         for (int row = 0; row < NB; ++row) {
             d[row][jj] = o[row * RS];
-            e[row][jj] = r[row * RS];
+            e[row][jj] = r[row * RRS];
         }
     }
     uint32_t ab[M::NQ];
@@ -1075,6 +1077,206 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Tiled scorer for V > 64 (256 views): the views are
+// split into groups of 64 and a work item is (tile chunk, view group).  The
+// workgroup stages the tile's window region of its 64 views only
+// ([row][quad][64] dwords, 36.9 KB at wid 5), one lane per view of the group
+// as in k_score_tiled3.  The reference view R is generally in another group,
+// so each wave copies the current candidate's 11x4 reference quads from the
+// stack into a private LDS slot (one dword per lane, prefetched one
+// candidate ahead) and reads them from there as broadcasts.  A group writes
+// its own mask word (64 views = one word) and a partial (count, sum of
+// ncc*(n-1)); k_group_finalize adds the partials.
+// ---------------------------------------------------------------------------
+constexpr int kTGThreads = 256, kTGWaves = kTGThreads / 64;
+
+template <int WID>
+__global__ __launch_bounds__(kTGThreads, 3) void k_score_tiledg(const SceneDev sc, const ScoreArgs a,
+                                                                const TiledArgs t) {
+    using G = TileGeom<WID>;
+    constexpr int NB = 2 * WID + 1;
+    constexpr int NPX = NB * NB;
+    constexpr int QS = 64;
+    constexpr int RS = G::NQ * QS;
+    constexpr int SLOT = NB * 4;                 // reference quads per wave: [row][4]
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int V = sc.V;
+    const int NG = t.groups;
+    const int n_items = t.item_off[t.ntiles] * NG;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const MomEntry* __restrict__ mom = sc.mom[WID];
+    uint64_t* o_mask = (uint64_t*)(lds + G::ROWS * RS);
+    double* o_sum = (double*)(o_mask + t.chunk);
+    int32_t* o_cnt = (int32_t*)(o_sum + t.chunk);
+    int32_t* o_idx = o_cnt + t.chunk;
+    uint32_t* slot = (uint32_t*)(o_idx + t.chunk) + wave * SLOT;
+    __shared__ int s_item;
+    // the reference quads of candidate pk (lanes < SLOT; zero past the last quad)
+    auto ref_quads = [&](int pk) -> uint32_t {
+        uint32_t v = 0;
+        if (lane < SLOT) {
+            const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
+            const int row = lane >> 2, gq = ((q - WID) >> 2) + (lane & 3);
+            if (gq < sc.Wq)
+                v = *(const uint32_t*)(sc.stack + (int64_t)(r - WID + row) * sc.row_bytes +
+                                       (int64_t)gq * V * 4 + R * 4);
+        }
+        return v;
+    };
+    for (;;) {
+        if (threadIdx.x == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
+        __syncthreads();
+        const int gitem = __builtin_amdgcn_readfirstlane(s_item);
+        if (gitem >= n_items) break;
+        // the NG groups of one chunk are consecutive items: they run at the
+        // same time and share the chunk's candidate list and moment rows in L2
+        const int item = gitem / NG, g = gitem - item * NG;
+        const int vb = 64 * g, nv = min(64, V - vb);
+        int lo = 0, hi = t.ntiles;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (t.item_off[mid] <= item) lo = mid; else hi = mid;
+        }
+        const int tile = lo;
+        const int chunk = item - t.item_off[tile];
+        const int cb = t.tile_off[tile] + chunk * t.chunk;
+        const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int y0 = ty * kTH - WID;
+        const int kq0 = tx * (kTW / 4) + G::KQ0;
+        {
+            const int cpq = nv >> 2, cpr = G::NQ * cpq, total = G::ROWS * cpr;
+            for (int base = 0; base < total; base += 8 * kTGThreads) {
+                uint4 buf[8];
+                int dst[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = base + u * kTGThreads + (int)threadIdx.x;
+                    dst[u] = -1;
+                    buf[u] = make_uint4(0, 0, 0, 0);
+                    if (k < total) {
+                        const int ry = k / cpr, rem = k - ry * cpr;
+                        const int kq = rem / cpq, vq = rem - kq * cpq;
+                        const int y = y0 + ry, gq = kq0 + kq;
+                        if (y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                            buf[u] = *(const uint4*)(sc.stack + (int64_t)y * sc.row_bytes +
+                                                      (int64_t)gq * V * 4 + (vb + 4 * vq) * 4);
+                        dst[u] = (ry * G::NQ + kq) * QS + vq * 4;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (dst[u] >= 0) *(uint4*)(lds + dst[u]) = buf[u];
+            }
+        }
+        auto sload = [](const int2* p) -> int2 {
+            const unsigned long long v = *(const __attribute__((address_space(4))) unsigned long long*)p;
+            return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+        };
+        auto pix = [&](int pk) -> int64_t { return (int64_t)((pk >> 11) & 0x7ff) * sc.W + (pk & 0x7ff); };
+        int2 cur = cb + wave < ce ? sload(t.sorted + cb + wave) : make_int2(0, 0);
+        MomEntry mb_cur{0.0, 0u}, ma_cur{0.0, 0u};
+        if (cb + wave < ce) {
+            if (lane < nv) mb_cur = load_mom(mom, pix(cur.y) * V + vb + lane);
+            ma_cur = load_mom(mom, pix(cur.y) * V + ((cur.y >> 22) & 0x3ff));
+            const uint32_t rq = ref_quads(cur.y);
+            if (lane < SLOT) slot[lane] = rq;
+        }
+        __syncthreads();   // region image complete
+        for (int j = cb + wave; j < ce; j += kTGWaves) {
+            const bool more = j + kTGWaves < ce;
+            const int2 nxt = more ? sload(t.sorted + j + kTGWaves) : make_int2(0, 0);
+            MomEntry mb_nxt{0.0, 0u}, ma_nxt{0.0, 0u};
+            uint32_t rq_nxt = 0;
+            if (more) {
+                if (lane < nv) mb_nxt = load_mom(mom, pix(nxt.y) * V + vb + lane);
+                ma_nxt = load_mom(mom, pix(nxt.y) * V + ((nxt.y >> 22) & 0x3ff));
+                rq_nxt = ref_quads(nxt.y);
+            }
+            const int pk = cur.y;
+            const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
+            const int q0 = q - WID, o = q0 & 3;
+            const int k0 = (q0 >> 2) - kq0;
+            const MomEntry mb = mb_cur, ma = ma_cur;
+            const uint32_t* basep = lds + (r - WID - y0) * RS + k0 * QS + lane;
+            uint32_t Sab = 0;
+            if (lane < nv) {
+                switch (o) {
+                    case 0: Sab = sab_rows<WID, 0, RS, QS, 4, 1>(basep, slot); break;
+                    case 1: Sab = sab_rows<WID, 1, RS, QS, 4, 1>(basep, slot); break;
+                    case 2: Sab = sab_rows<WID, 2, RS, QS, 4, 1>(basep, slot); break;
+                    default: Sab = sab_rows<WID, 3, RS, QS, 4, 1>(basep, slot); break;
+                }
+            }
+            // the next candidate's reference quads replace this one's: the wave's
+            // LDS operations complete in program order, after the reads above
+            if (more && lane < SLOT) slot[lane] = rq_nxt;
+            const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma.sb, mb.sb));
+            const bool live = lane < nv && vb + lane != R && mb.w > 0.0 && ma.w > 0.0;
+            bool pass = false, guard = false;
+            double ncc = 0.0;
+            if (live) {
+                if (a.thr >= 0.01) {
+                    const double tk = a.thr * (double)(NPX - 1);
+                    const double z = ((double)num * ((double)NPX * ma.w)) * mb.w;
+                    guard = fabs(z - tk) <= 1e-8 * tk;
+                    pass = z > tk;
+                    ncc = z;
+                } else {
+                    const int32_t db = mom_db(mb), da = mom_db(ma);
+                    ncc = ((double)num * (double)NPX) /
+                          ((double)(NPX - 1) * sqrt((double)da * (double)db));
+                    guard = fabs(ncc - a.thr) <= kGuard;
+                    pass = ncc > a.thr;
+                    ncc *= (double)(NPX - 1);
+                }
+            }
+            if (__ballot(guard) != 0 && lane == 0) t.fix_list[atomicAdd(t.fix_count, 1)] = cur.x;
+            const uint64_t m = __ballot(pass);
+            const int cnt = __popcll(m);
+            const double sum = (a.avg && cnt) ? wave_sum_dpp(pass ? ncc : 0.0) : 0.0;
+            const int sl = j - cb;
+            if (lane == 0) {
+                o_mask[sl] = m;
+                o_sum[sl] = sum;
+                o_cnt[sl] = cnt;
+                o_idx[sl] = cur.x;
+            }
+            cur = nxt;
+            mb_cur = mb_nxt;
+            ma_cur = ma_nxt;
+        }
+        __syncthreads();
+        const int words = (V + 63) >> 6;
+        for (int k = threadIdx.x; k < ce - cb; k += blockDim.x) {
+            const int64_t i = o_idx[k];
+            a.mask[i * words + g] = o_mask[k];
+            t.part_cnt[i * NG + g] = o_cnt[k];
+            t.part_sum[i * NG + g] = o_sum[k];
+        }
+        __syncthreads();
+    }
+}
+
+// count and avg_ncc_score of every scored candidate from its view groups'
+// partials (same scaling as k_score_tiled3: sum * (1/cnt) * (1/(n-1)))
+__global__ void k_group_finalize(const ScoreArgs a, const TiledArgs t, int npx) {
+    const int NG = t.groups;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (t.cand_key[i] < 0) continue;     // invalid window: k_bin wrote the outputs
+        int cnt = 0;
+        double sum = 0.0;
+        for (int g = 0; g < NG; ++g) {
+            cnt += t.part_cnt[i * NG + g];
+            sum += t.part_sum[i * NG + g];
+        }
+        a.count[i] = cnt;
+        if (a.avg) a.avg[i] = cnt ? sum * ((1.0 / (double)cnt) * (1.0 / (double)(npx - 1))) : 0.0;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // MFMA scorer.  S_ab of a candidate (pixel p, reference view R) against every
@@ -1692,7 +1894,7 @@ __global__ __launch_bounds__(kM2Threads, 3) void k_score_mfma2(const SceneDev sc
 // Re-scores the candidates k_score_tiled3 flagged (a view decision inside the
 // guard band) with the direct scorer, whose guard lanes take the numpy-order
 // ctNcc; overwrites their mask/count/avg.  One wave per flagged candidate.
-template <int WID>
+template <int WID, int NS = 1>
 __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t) {
     const int nfix = *t.fix_count;
@@ -1701,8 +1903,9 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
         const int64_t cand = __builtin_amdgcn_readfirstlane(t.fix_list[k]);
         const int pk = __builtin_amdgcn_readfirstlane(t.cand_pk[cand]);
         const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
-        wave_score<WID, 1>(sc, R, q, r, a.thr, a.mask + cand, a.count + cand,
-                           a.avg ? a.avg + cand : nullptr, a.exact_hits);
+        const int words = (sc.V + 63) >> 6;
+        wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * words, a.count + cand,
+                            a.avg ? a.avg + cand : nullptr, a.exact_hits);
     }
 }
 
@@ -1948,6 +2151,38 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// V > 64: bin/scan/scatter as for k_score_tiled3, then the view-group scorer,
+// the partials' reduction and the guard-band re-score (direct path, NS slots).
+template <int WID>
+int launch_score_tiledg_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s,
+                          hipEvent_t ev0, hipEvent_t ev1) {
+    using G = TileGeom<WID>;
+    if (a->n == 0) return 0;
+    if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || sc->V > 256 || t->chunk > kChunk ||
+        t->groups != (sc->V + 63) / 64 || t->part_cnt == nullptr || t->part_sum == nullptr ||
+        t->tw != kTW || t->th != kTH)
+        return -3;
+    if (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess) return -1;
+    const int64_t per_block = (int64_t)kBinBlock * kBinPer;
+    const int nbin = (int)((a->n + per_block - 1) / per_block);
+    hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, *t);
+    const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
+    const size_t lds = (size_t)G::ROWS * G::NQ * 64 * 4 + (size_t)t->chunk * (8 + 8 + 4 + 4) +
+                       (size_t)kTGWaves * (2 * WID + 1) * 4 * 4;
+    {
+        TimedLaunch tl(s, ev0, ev1);
+        hipLaunchKernelGGL((k_score_tiledg<WID>), dim3(kTiledBlocks), dim3(kTGThreads), lds, s, *sc, *a, *t);
+    }
+    hipLaunchKernelGGL(k_group_finalize, dim3(nb), dim3(256), 0, s, *a, *t, (2 * WID + 1) * (2 * WID + 1));
+    if (sc->V <= 128)
+        hipLaunchKernelGGL((k_score_fix<WID, 2>), dim3(64), dim3(256), 0, s, *sc, *a, *t);
+    else
+        hipLaunchKernelGGL((k_score_fix<WID, 4>), dim3(64), dim3(256), 0, s, *sc, *a, *t);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <int WID>
 int launch_expand_w(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, hipStream_t s) {
     const int64_t blocks = (a->n + 3) / 4;
@@ -2021,7 +2256,16 @@ extern "C" void mvs_tiled_geometry(int W, int H, int mfma, int* tw, int* th, int
 extern "C" int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t,
                                       int wid, int variant, hipStream_t s, hipEvent_t ev0,
                                       hipEvent_t ev1) {
-    if (sc->V > 64) return -3;
+    if (sc->V > 64) {
+        switch (wid) {
+            case 1: return launch_score_tiledg_w<1>(sc, a, t, s, ev0, ev1);
+            case 2: return launch_score_tiledg_w<2>(sc, a, t, s, ev0, ev1);
+            case 3: return launch_score_tiledg_w<3>(sc, a, t, s, ev0, ev1);
+            case 4: return launch_score_tiledg_w<4>(sc, a, t, s, ev0, ev1);
+            case 5: return launch_score_tiledg_w<5>(sc, a, t, s, ev0, ev1);
+            default: return -2;
+        }
+    }
     switch (wid) {
         case 1: return launch_score_tiled_w<1>(sc, a, t, variant, s, ev0, ev1);
         case 2: return launch_score_tiled_w<2>(sc, a, t, variant, s, ev0, ev1);

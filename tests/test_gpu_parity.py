@@ -264,9 +264,11 @@ def test_stage_empty_and_ragged_tracks(ctx, oracle_scene, seeds):
     assert np.array_equal(allp, oall)
 
 
-@pytest.mark.parametrize("V", [5, 100, 256])
+@pytest.mark.parametrize("V", [5, 100, 102, 192, 256])
 def test_view_count_variants(pkg, orc, V):
-    """Lane-slot layouts: V < 64, one extra slot, and the 4-slot 256-view case."""
+    """Lane-slot layouts: V < 64, one extra slot, and the 4-slot 256-view case;
+    3000 candidates take the tiled scorers (k_score_tiled3, or the view-group
+    k_score_tiledg for V > 64 with V % 4 == 0; V = 102 stays on k_score)."""
     syn = pkg.synthetic
     H, W = 96, 128
     rgb, K, R, t = syn.ring_scene(V=V, H=H, W=W, seed=V)
