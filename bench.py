@@ -6,8 +6,9 @@ of 2^20 synthetic candidate patches per GPU (reference view, sub-pixel pixel,
 depth 0.60-0.72 m; seed 0 + rank), every candidate photo-tested against all 48
 views with the reference's 11x11 window (wid=5, MVS2.py:64/69) at MIN_NCC 0.7.
 A step = score the sweep on the GPU (inputs resident in HBM) + compact the
-accepted candidates (|V| >= 3) + RCCL all-gather of the accepted records
-across ranks (the sweep's exchange step; skipped at N=1).
+accepted candidates (|V| >= 3: accept bitmap + their V masks) + RCCL
+all-gather of that accepted set across ranks (the sweep's exchange step;
+skipped at N=1).
 
 python bench.py [--gpus N --steps K --warmup W --n CANDS --wid 5]
 N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -111,10 +112,10 @@ def main():
         if evs is not None:
             evs[1].record(stream)
         if world > 1:
-            # the sweep's exchange (parallel.py): accepted records to every rank
-            rec = par.pack_accepted(rank * n, count, mask, xy, vlb)
-            allrec = par.all_gather_records(rec)
-            gathered["n"] = int(allrec.shape[0])
+            # the sweep's exchange (parallel.py): every rank's accepted set
+            # (accept bitmap + V masks; count = popcount, centroids known) to every rank
+            blocks = par.all_gather_compact(par.pack_compact(count, mask, vlb))
+            gathered["n"] = sum((b.numel() - 1 - (n + 63) // 64) // words for b in blocks)
 
     def timed(wid, steps, warmup):
         for _ in range(warmup):

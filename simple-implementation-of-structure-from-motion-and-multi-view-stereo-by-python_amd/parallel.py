@@ -72,6 +72,72 @@ def unpack_records(rec, words):
     return idx, count, mask, xy
 
 
+# Compact form of a rank's accepted set (the bench's per-sweep exchange): one
+# int64 block [k, accept bitmap (ceil(n/64) words, bit i = candidate i),
+# masks of the k accepted candidates (k*words)].  count = popcount(mask) and
+# the candidates' centroids / projections are known to every rank (the
+# sweep's candidate list is), so the bitmap and the masks are the whole
+# accepted set at 8 B per accepted candidate plus n/8 B -- 5x less than the
+# explicit records above, which matters on xGMI at N = 8.
+def pack_compact(count, mask, vlb):
+    n = count.numel()
+    words = mask.shape[1]
+    nbw = (n + 63) // 64
+    acc = count >= vlb
+    a = acc.to(torch.int64)
+    if nbw * 64 != n:
+        a = torch.cat([a, a.new_zeros(nbw * 64 - n)])
+    sh = torch.arange(64, dtype=torch.int64, device=count.device)
+    bits = (a.view(nbw, 64) << sh).sum(1)            # distinct bits: the sum is their OR
+    masks = mask[acc].reshape(-1)
+    k = masks.numel() // max(words, 1)
+    head = torch.full((1,), k, dtype=torch.int64, device=count.device)
+    return torch.cat([head, bits, masks.view(torch.int64)])
+
+
+def all_gather_compact(block, group=None):
+    """All-gather the ranks' compact blocks -> list of blocks in rank order."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return [block]
+    k = torch.tensor([block.numel()], dtype=torch.int64, device=block.device)
+    ks = torch.empty(world, dtype=torch.int64, device=block.device)
+    dist.all_gather_into_tensor(ks, k, group=group)
+    sizes = ks.tolist()
+    kmax = max(sizes)
+    buf = torch.zeros(kmax, dtype=torch.int64, device=block.device)
+    buf[:block.numel()] = block
+    flat = torch.empty(world * kmax, dtype=torch.int64, device=block.device)
+    dist.all_gather_into_tensor(flat, buf, group=group)
+    return [flat[r * kmax: r * kmax + sizes[r]] for r in range(world)]
+
+
+_POP8 = None
+
+
+def unpack_compact(blocks, n, words):
+    """Compact blocks of ranks 0..world-1 (slices of n candidates each, rank r's
+    candidate i = global index r*n + i) -> (index, count, mask) in global order."""
+    global _POP8
+    idx, cnt, msk = [], [], []
+    nbw = (n + 63) // 64
+    for r, b in enumerate(blocks):
+        k = int(b[0].item())
+        bits = b[1:1 + nbw]
+        sh = torch.arange(64, dtype=torch.int64, device=b.device)
+        flags = ((bits.unsqueeze(1) >> sh) & 1).reshape(-1)[:n].bool()
+        ii = torch.nonzero(flags).squeeze(1) + r * n
+        m = b[1 + nbw:1 + nbw + k * words].reshape(k, words)
+        if _POP8 is None or _POP8.device != b.device:
+            _POP8 = torch.tensor([bin(v).count("1") for v in range(256)], dtype=torch.int32,
+                                 device=b.device)
+        c = _POP8[m.contiguous().view(torch.uint8).long()].reshape(k, -1).sum(1).to(torch.int32)
+        idx.append(ii)
+        cnt.append(c)
+        msk.append(m)
+    return torch.cat(idx), torch.cat(cnt), torch.cat(msk)
+
+
 def sharded_sweep(score_fn, c, ref, vlb, words, group=None):
     """Score the sweep [c, ref] (all ranks pass the same full batch) by slices and
     exchange the accepted records.  score_fn(c_slice, ref_slice) -> (xy, mask, count)

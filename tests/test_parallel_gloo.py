@@ -160,3 +160,50 @@ def test_stage_sharded_driver_gloo(tmp_path, world):
     mp.spawn(_stage_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert np.load(tmp_path / f"s{r}.npy").tolist() == [5, 8, 3, 1]
+
+
+def _compact_worker(rank, world, port, n, words, out_dir):
+    import importlib
+    sys.path.insert(0, REPO)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    par = importlib.import_module(PKG_NAME + ".parallel")
+    rng = np.random.default_rng(100 + rank)          # this rank's own sweep slice (seed = rank)
+    mask = rng.integers(0, 2**63, (n, words), dtype=np.int64)
+    mask[rng.random((n, words)) < 0.5] = 0
+    mask[:, 0] |= np.int64(-2**63) * (rng.random(n) < 0.3)   # bit 63 set on some masks
+    cnt = np.array([sum(bin(int(w) & (2**64 - 1)).count("1") for w in row) for row in mask], np.int32)
+    blk = par.pack_compact(torch.from_numpy(cnt), torch.from_numpy(mask), 3)
+    blocks = par.all_gather_compact(blk)
+    idx, count, m = par.unpack_compact(blocks, n, words)
+    np.savez(os.path.join(out_dir, f"c{rank}.npz"), idx=idx.numpy(), count=count.numpy(),
+             mask=m.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,words", [(2, 1000, 1), (3, 130, 4)])
+def test_compact_exchange_gloo(tmp_path, world, n, words):
+    """The bench's per-sweep exchange (bitmap + masks of accepted candidates):
+    every rank rebuilds every rank's accepted (index, count, mask)."""
+    mp.spawn(_compact_worker, args=(world, _free_port(), n, words, str(tmp_path)), nprocs=world,
+             join=True)
+    exp_i, exp_c, exp_m = [], [], []
+    for r in range(world):
+        rng = np.random.default_rng(100 + r)
+        mask = rng.integers(0, 2**63, (n, words), dtype=np.int64)
+        mask[rng.random((n, words)) < 0.5] = 0
+        mask[:, 0] |= np.int64(-2**63) * (rng.random(n) < 0.3)
+        cnt = np.array([sum(bin(int(w) & (2**64 - 1)).count("1") for w in row) for row in mask])
+        acc = np.nonzero(cnt >= 3)[0]
+        exp_i.append(acc + r * n)
+        exp_c.append(cnt[acc])
+        exp_m.append(mask[acc])
+    exp_i, exp_c, exp_m = np.concatenate(exp_i), np.concatenate(exp_c), np.concatenate(exp_m)
+    assert len(exp_i) > 0
+    for r in range(world):
+        z = np.load(tmp_path / f"c{r}.npz")
+        assert np.array_equal(z["idx"], exp_i)
+        assert np.array_equal(z["count"], exp_c)
+        assert np.array_equal(z["mask"], exp_m)
