@@ -53,6 +53,9 @@ def load_scene():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group backend for N > 1 (nccl = RCCL over xGMI; gloo only "
+                         "to rehearse the multi-rank path with several ranks on one GPU)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=1 << 20, help="candidates per GPU per sweep")
@@ -80,7 +83,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     pkg = importlib.import_module(PKG_NAME)
     par = importlib.import_module(PKG_NAME + ".parallel")
 
@@ -216,7 +222,7 @@ def main():
             "config": {"workload": f"{'dinoRing' if a.scene == 'dino' else 'ring'} {V}x{W}x{H}, "
                                    f"one expansion sweep of {n} candidates per GPU, "
                                    f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
-                                   f"MIN_NCC {a.thr}, accepted records all-gathered",
+                                   f"MIN_NCC {a.thr}, accepted set all-gathered",
                        "global_batch": n * world, "wid": a.wid, "views": V,
                        "parallelism": f"candidate-queue shards x{world} (RCCL all-gather)"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
