@@ -75,6 +75,11 @@ def load(path=None):
         raise RuntimeError(
             f"libmvs_amd.so not found at {path}: build it with __graft_entry__.build() "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    # torch first: its bundled HIP runtime (SONAME libamdhip64.so.7) is then
+    # the one libmvs_amd.so's NEEDED entry binds to, so torch tensors, torch
+    # streams and the library share one runtime.  Loaded the other way round
+    # the process would hold two HIP runtimes and torch.cuda would not start.
+    import torch  # noqa: F401
     try:
         lib = ctypes.CDLL(path)
     except OSError as e:

@@ -1086,7 +1086,8 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
 // as in k_score_tiled3.  The reference view R is generally in another group,
 // so each wave copies the current candidate's 11x4 reference quads from the
 // stack into a private LDS slot (one dword per lane, prefetched one
-// candidate ahead) and reads them from there as broadcasts.  A group writes
+// candidate ahead) and reads them from there as broadcasts.  (Masking the
+// slot once instead of per lane measured 12 % slower: 2.96 vs 2.65 ms.)  A group writes
 // its own mask word (64 views = one word) and a partial (count, sum of
 // ncc*(n-1)); k_group_finalize adds the partials.
 // ---------------------------------------------------------------------------

@@ -405,3 +405,29 @@ def test_stage_sharded_ranks_emulated(pkg, dino, seeds, world):
         ini_r, allp_r, st_r = res[-1]
         assert st_r["tests"] == j["stats"]["tests"]
         assert hashlib.sha256(np.ascontiguousarray(allp_r, "<f8").tobytes()).hexdigest() == j["sha256_all"]
+
+
+def test_one_hip_runtime_whatever_the_import_order(tmp_path):
+    """Loading the library before torch must still leave ONE HIP runtime in the
+    process (torch's), so torch.cuda works and device pointers are shared."""
+    import subprocess
+    import sys
+    from conftest import PKG_NAME, REPO
+    code = (
+        "import importlib, sys\n"
+        f"sys.path.insert(0, {REPO!r})\n"
+        f"pkg = importlib.import_module({PKG_NAME!r})\n"
+        "pkg._lib.load()\n"
+        "import numpy as np\n"
+        "rgb = np.zeros((2, 32, 32, 3), np.uint8)\n"
+        "K = np.tile(np.array([[50., 0, 16], [0, 50., 16], [0, 0, 1]]), (2, 1, 1))\n"
+        "R = np.tile(np.eye(3), (2, 1, 1)); t = np.tile(np.array([0., 0, 1]), (2, 1))\n"
+        "ctx = pkg.MvsContext(rgb, K, R, t, device=0)\n"
+        "import torch\n"
+        "assert torch.cuda.is_available()\n"
+        "maps = [l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l]\n"
+        "assert len(set(maps)) == 1, set(maps)\n"
+        "x = torch.ones(4, device='cuda:0'); assert float(x.sum()) == 4.0\n"
+        "ctx.close(); print('ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
