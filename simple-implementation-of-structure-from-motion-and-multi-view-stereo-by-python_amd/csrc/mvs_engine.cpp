@@ -399,7 +399,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         TiledArgs t{};
         mvs_tiled_geometry(ctx->W, ctx->H, mfma ? 1 : 0, &t.tw, &t.th, &t.ntx, &t.nty);
         const int ntiles = t.ntx * t.nty;
-        ctx->t_tiles.ensure((size_t)3 * (ntiles + 2));
+        ctx->t_tiles.ensure((size_t)3 * (ntiles + 2) + 8);
         const int groups = grouped ? (ctx->V + 63) / 64 : 1;
         ctx->t_cand.ensure((size_t)(5 + groups) * n);   // fix_list: one entry per (candidate, group)
         t.ntiles = ntiles;
@@ -420,6 +420,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.cand_pk = ctx->t_cand.p + 2 * n;
         t.sorted = (int2*)(ctx->t_cand.p + 3 * n);
         t.fix_list = ctx->t_cand.p + 5 * n;
+        t.xq = ctx->t_tiles.p + 3 * (ntiles + 2);
         hipEvent_t e0, e1;
         ctx->next_events(&e0, &e1);
         if (mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, variant, s, e0, e1) != 0)

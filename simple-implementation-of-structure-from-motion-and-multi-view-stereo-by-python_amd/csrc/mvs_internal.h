@@ -90,6 +90,7 @@ struct TiledArgs {
     int groups;
     int32_t* part_cnt;         // n*groups
     double* part_sum;          // n*groups
+    int32_t* xq;               // 8 work-queue heads, one per XCD label (blockIdx % 8)
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).

@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
 // ([row][quad][64] dwords, 36.9 KB at wid 5), one lane per view of the group
 // as in k_score_tiled3.  The reference view R is generally in another group,
 // so each wave copies the current candidate's 11x4 reference quads from the
-// stack into a private LDS slot (one dword per lane, prefetched one
+// view-major copy gv into a private LDS slot (one dword per lane, prefetched one
 // candidate ahead) and reads them from there as broadcasts.  (Masking the
 // slot once instead of per lane measured 12 % slower: 2.96 vs 2.65 ms.)  A group writes
 // its own mask word (64 views = one word) and a partial (count, sum of
@@ -1105,7 +1105,13 @@ __global__ __launch_bounds__(kTGThreads, 3) void k_score_tiledg(const SceneDev s
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int V = sc.V;
     const int NG = t.groups;
-    const int n_items = t.item_off[t.ntiles] * NG;
+    // XCD-aware work queues: blocks b and b + 8 share an XCD (and its L2), so
+    // queue x = blockIdx % 8 hands out the chunks c = x (mod 8), all NG view
+    // groups of a chunk in a row: the groups of one chunk run on one XCD and
+    // share its L2 lines (candidate list, reference rows of gv).
+    const int xq = blockIdx.x & 7;
+    const int n_chunks = t.item_off[t.ntiles];
+    const int n_items = n_chunks > xq ? ((n_chunks - xq + 7) >> 3) * NG : 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const MomEntry* __restrict__ mom = sc.mom[WID];
     uint64_t* o_mask = (uint64_t*)(lds + G::ROWS * RS);
@@ -1114,26 +1120,26 @@ __global__ __launch_bounds__(kTGThreads, 3) void k_score_tiledg(const SceneDev s
     int32_t* o_idx = o_cnt + t.chunk;
     uint32_t* slot = (uint32_t*)(o_idx + t.chunk) + wave * SLOT;
     __shared__ int s_item;
-    // the reference quads of candidate pk (lanes < SLOT; zero past the last quad)
+    // the reference quads of candidate pk (lanes < SLOT), from the view-major
+    // copy gv: a window row's 4 quads are 16 contiguous bytes there (one cache
+    // line per row instead of one per quad in the view-interleaved stack);
+    // the row pitch Wp >= 4 (W/4 + 1) keeps the last quad in bounds
     auto ref_quads = [&](int pk) -> uint32_t {
         uint32_t v = 0;
         if (lane < SLOT) {
             const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
             const int row = lane >> 2, gq = ((q - WID) >> 2) + (lane & 3);
-            if (gq < sc.Wq)
-                v = *(const uint32_t*)(sc.stack + (int64_t)(r - WID + row) * sc.row_bytes +
-                                       (int64_t)gq * V * 4 + R * 4);
+            v = *(const uint32_t*)(sc.gv + ((int64_t)R * sc.H + (r - WID + row)) * sc.Wp + 4 * gq);
         }
         return v;
     };
     for (;;) {
-        if (threadIdx.x == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
+        if (threadIdx.x == 0) s_item = atomicAdd(&t.xq[xq], 1);
         __syncthreads();
-        const int gitem = __builtin_amdgcn_readfirstlane(s_item);
-        if (gitem >= n_items) break;
-        // the NG groups of one chunk are consecutive items: they run at the
-        // same time and share the chunk's candidate list and moment rows in L2
-        const int item = gitem / NG, g = gitem - item * NG;
+        const int k = __builtin_amdgcn_readfirstlane(s_item);
+        if (k >= n_items) break;
+        const int kc = k / NG, g = k - kc * NG;
+        const int item = xq + 8 * kc;
         const int vb = 64 * g, nv = min(64, V - vb);
         int lo = 0, hi = t.ntiles;
         while (hi - lo > 1) {
@@ -2163,13 +2169,16 @@ int launch_score_tiledg_w(const SceneDev* sc, const ScoreArgs* a, const TiledArg
         t->groups != (sc->V + 63) / 64 || t->part_cnt == nullptr || t->part_sum == nullptr ||
         t->tw != kTW || t->th != kTH)
         return -3;
+    if (t->xq == nullptr) return -3;
     if (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess) return -1;
+    if (hipMemsetAsync(t->xq, 0, sizeof(int32_t) * 8, s) != hipSuccess) return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);
     hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, *t);
     const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
+    static_assert(kTiledBlocks % 8 == 0, "queue labels need a multiple of 8 blocks");
     const size_t lds = (size_t)G::ROWS * G::NQ * 64 * 4 + (size_t)t->chunk * (8 + 8 + 4 + 4) +
                        (size_t)kTGWaves * (2 * WID + 1) * 4 * 4;
     {
