@@ -164,6 +164,37 @@ int mvs_rodrigues_roundtrip(const double* R, double* Rp);
 int mvs_triangulate(const double* P1, const double* P2, const double* x1, const double* x2,
                     double* X4);
 
+/* ---- SfM front-end: the producer of the stage's seed tracks ----
+ * (BASELINE config 5: HarrisFeatures + SFM.py feeding MVS; the reference's
+ * default SfM matcher is OpenCV ORB/FLANN/RANSAC, SFM.py:56, utils.py:160-232)
+ *
+ * getHarrisPoints(imgs[view]) (HarrisFeatures.py:135-161) on the GPU:
+ * cv2.cornerHarris(gray, 2, 3, 0.04), 3x3 dilate, keep > float32(0.01) * max,
+ * np.where row-major order.  out: [col, row] int32 pairs (host), at most cap
+ * of them; *n_out = the total (call with cap 0 to size the buffer). */
+int mvs_harris_points(mvs_ctx* ctx, int view, int32_t* out, int64_t cap, int64_t* n_out);
+
+/* MatchTwoSided(getDescFeatures(imgs[view_a], pts_a, wid),
+ *               getDescFeatures(imgs[view_b], pts_b, wid), thr)
+ * (HarrisFeatures.py:15-67) on the GPU.  pts_* are [row, col] int32 (host),
+ * all inside getDescFeatures' bounds (else MVS_E_ARG).  m12[i] = j when j is
+ * i's best match and i is j's, else -1; best12 / best21 (may be NULL): the
+ * one-sided argmax of ncc > thr (ties -> smallest index, -1 when no ncc
+ * exceeds thr; numpy's argsort leaves both cases implementation-defined). */
+int mvs_match_two_sided(mvs_ctx* ctx, int view_a, const int32_t* pts_a, int64_t n_a, int view_b,
+                        const int32_t* pts_b, int64_t n_b, int wid, double thr, int32_t* m12,
+                        int32_t* best12, int32_t* best21);
+
+/* One image pair of StructureFromMotion's loop (SFM.py:60-80), host:
+ * P = K [R | t] per view (getProjectionMatrix), cv2.triangulatePoints of
+ * the float32 correspondences q (view A) / tr (view B) (float32 result),
+ * point = X / w; keep[i] = 1 when w != 0 and both projectPoint residuals
+ * (float32 norm) are <= max_err (MIN_REPROJECTION_ERROR).  pt: float32 (n, 3).
+ * K, R row-major 3x3, t 3 doubles. */
+int mvs_sfm_pair(const double* KA, const double* RA, const double* tA, const double* KB,
+                 const double* RB, const double* tB, int64_t n, const float* q, const float* tr,
+                 double max_err, float* pt, uint8_t* keep);
+
 #ifdef __cplusplus
 }
 #endif

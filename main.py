@@ -8,10 +8,13 @@ libmvs_amd.so and writes initial_patches.ply / all_patches.ply in the working
 directory, like the reference.  Under torchrun (one process per GPU) the
 expansion sweeps are sharded over the GPUs:
 
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py -img_p ... -seeds ...  The reference's SfM stage (ORB + FLANN +
-RANSAC through OpenCV, SFM.py) is not part of this build: its output -- the
-GlobalSet tracks -- is read from -seeds (npz with track_off, obs_view, obs_xy,
-the format tests/golden/make_seeds.py writes).
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py -img_p ... -seeds ...
+
+Tracks: without -seeds, StructureFromMotion (SFM.py:47-88) runs first with the
+reference's Harris/NCC features (HarrisFeatures.py) matched on the GPU in
+place of OpenCV's ORB + FLANN + RANSAC (absent from this image); with -seeds
+FILE.npz (track_off, obs_view, obs_xy, the format tests/golden/make_seeds.py
+and -save_tracks write) the tracks are read instead.
 """
 import importlib
 import os
@@ -23,7 +26,7 @@ PKG_NAME = "simple-implementation-of-structure-from-motion-and-multi-view-stereo
 sys.path.insert(0, REPO)
 
 
-def main(args):
+def main(args, threshold=0.01, MIN_REPROJECTION_ERROR=0.3):
     mvs = importlib.import_module(PKG_NAME)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
@@ -36,9 +39,20 @@ def main(args):
         if not dist.is_initialized():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     imgs = mvs.read_imgs(args)
-    if not args.seeds:
-        raise RuntimeError("no SfM tracks: this build has no OpenCV SfM stage; pass -seeds FILE.npz")
-    global_set = mvs.SeedSet.load(args.seeds)
+    if args.seeds:
+        global_set = mvs.SeedSet.load(args.seeds)
+    else:
+        # SfM.StructureFromMotion (main.py:28) with the Harris/NCC front-end on
+        # the GPU in place of OpenCV's ORB/FLANN/RANSAC (sfm.py)
+        global_set = mvs.sfm.GlobalSet(threshold=threshold)
+        st = mvs.sfm.StructureFromMotion(imgs, global_set, args, MIN_REPROJECTION_ERROR)
+        n_obs, n_pts, _ = global_set.getInfo()
+        print(f"SfM: {st['pairs']} pairs, {st['correspondences']} correspondences, "
+              f"{st['kept']} triangulated, {n_pts} tracks / {n_obs} observations")
+    if args.save_tracks and (world == 1 or int(os.environ.get("RANK", "0")) == 0):
+        import numpy as np
+        off, view, xy = mvs.utils.tracks_to_arrays(global_set.getInfo()[2])
+        np.savez(args.save_tracks, track_off=off, obs_view=view, obs_xy=xy)
     mvs.DensePointsWithMVS2(imgs, global_set, args, max_pops=args.max_pops)
     st = mvs.MVS2.last_stats
     if world == 1 or int(os.environ.get("RANK", "0")) == 0:
@@ -59,6 +73,8 @@ if __name__ == "__main__":
                         dest="seeds", default=None)
     parser.add_argument("-max_pops", help="expansion pop cap (<= 100000)", dest="max_pops",
                         default=100000, type=int)
+    parser.add_argument("-save_tracks", help="write the SfM tracks (npz) before the MVS stage",
+                        dest="save_tracks", default=None)
     args = parser.parse_args()
     try:
         main(args)

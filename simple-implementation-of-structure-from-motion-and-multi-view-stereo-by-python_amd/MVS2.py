@@ -26,11 +26,12 @@ def _device_index():
 
 
 def scene_context(imgs, par_K, par_r, par_t, device=None):
-    """MvsContext for (imgs, cameras), cached on the identity of imgs."""
-    key = (id(imgs), len(imgs), id(par_K), id(par_r), id(par_t))
+    """MvsContext for (imgs, cameras), cached on the identity of imgs and the
+    camera values (SfM and MVS each call read_pars, MVS2.py:178 / SFM.py:54)."""
+    K, R, t = pars_to_arrays(par_K, par_r, par_t, len(imgs))
+    key = (id(imgs), len(imgs), K.tobytes(), R.tobytes(), t.tobytes())
     ctx = _ctx_cache.get(key)
     if ctx is None:
-        K, R, t = pars_to_arrays(par_K, par_r, par_t, len(imgs))
         ctx = _lib.MvsContext(imgs, K, R, t, device=_device_index() if device is None else device)
         _ctx_cache.clear()
         _ctx_cache[key] = (ctx, imgs)

@@ -60,6 +60,12 @@ SIGNATURES = [
                                              _u64p, _i32p, _u8p]),
     ("mvs_rodrigues_roundtrip", ctypes.c_int, [_dp, _dp]),
     ("mvs_triangulate", ctypes.c_int, [_dp, _dp, _dp, _dp, _dp]),
+    ("mvs_harris_points", ctypes.c_int, [_vp, ctypes.c_int, _i32p, ctypes.c_int64, _i64p]),
+    ("mvs_match_two_sided", ctypes.c_int, [_vp, ctypes.c_int, _i32p, ctypes.c_int64, ctypes.c_int,
+                                           _i32p, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                           _i32p, _i32p, _i32p]),
+    ("mvs_sfm_pair", ctypes.c_int, [_dp, _dp, _dp, _dp, _dp, _dp, ctypes.c_int64, _fp, _fp,
+                                    ctypes.c_double, _fp, _u8p]),
 ]
 
 _lib = None
@@ -116,6 +122,22 @@ def rodrigues_roundtrip(R):
     out = np.empty(9)
     check(load().mvs_rodrigues_roundtrip(_p(R, _dp), _p(out, _dp)), what="rodrigues")
     return out.reshape(3, 3)
+
+
+def sfm_pair(KA, RA, tA, KB, RB, tB, q, tr, max_err):
+    """One pair of StructureFromMotion's loop (SFM.py:60-80), host C++:
+    (float32 points (n, 3), keep (n,) bool)."""
+    mats = [_c(m, np.float64).reshape(-1) for m in (KA, RA, tA, KB, RB, tB)]
+    q = _c(q, np.float32).reshape(-1, 2)
+    tr = _c(tr, np.float32).reshape(-1, 2)
+    n = len(q)
+    if len(tr) != n:
+        raise RuntimeError("query and train correspondences differ in length")
+    pt = np.empty((max(n, 1), 3), np.float32)
+    keep = np.empty(max(n, 1), np.uint8)
+    check(load().mvs_sfm_pair(*[_p(m, _dp) for m in mats], n, _p(q, _fp), _p(tr, _fp),
+                              float(max_err), _p(pt, _fp), _p(keep, _u8p)), None, "mvs_sfm_pair")
+    return pt[:n], keep[:n].astype(bool)
 
 
 def triangulate(P1, P2, x1, x2):
@@ -224,6 +246,33 @@ class MvsContext:
                                      ptr(avg) if avg is not None else None,
                                      stream if stream is not None else None)
         check(rc, self._h, "mvs_score_device")
+
+    def harris_points(self, view):
+        """getHarrisPoints(imgs[view]) (HarrisFeatures.py:135-161) on the GPU:
+        int32 (n, 2) [col, row] in np.where's row-major order."""
+        lib = load()
+        n = ctypes.c_int64(0)
+        check(lib.mvs_harris_points(self._h, int(view), None, 0, ctypes.byref(n)), self._h,
+              "mvs_harris_points")
+        out = np.empty((max(n.value, 1), 2), np.int32)
+        check(lib.mvs_harris_points(self._h, int(view), _p(out, _i32p), n.value, ctypes.byref(n)),
+              self._h, "mvs_harris_points")
+        return out[:n.value]
+
+    def match_two_sided(self, view_a, pts_a, view_b, pts_b, thr=0.5, wid=5):
+        """MatchTwoSided over getDescFeatures windows (HarrisFeatures.py:15-67) on the
+        GPU; pts_* [row, col] inside getDescFeatures' bounds.
+        Returns (m12, best12, best21) int32 (-1 = none)."""
+        a = _c(pts_a, np.int32).reshape(-1, 2)
+        b = _c(pts_b, np.int32).reshape(-1, 2)
+        m12 = np.empty(max(len(a), 1), np.int32)
+        b12 = np.empty(max(len(a), 1), np.int32)
+        b21 = np.empty(max(len(b), 1), np.int32)
+        check(load().mvs_match_two_sided(self._h, int(view_a), _p(a, _i32p), len(a), int(view_b),
+                                         _p(b, _i32p), len(b), int(wid), float(thr), _p(m12, _i32p),
+                                         _p(b12, _i32p), _p(b21, _i32p)),
+              self._h, "mvs_match_two_sided")
+        return m12[:len(a)], b12[:len(a)], b21[:len(b)]
 
     def expand_candidates(self, pc, pn, pxy, job_parent, job_view, job_di, cell_size=2,
                           scale=10.0, wid=5, min_ncc=0.7):

@@ -258,6 +258,30 @@ inline double fma_dot3(double a0, double a1, double a2, double b0, double b1, do
 
 inline int py_wrap(long i, long n) { return (int)(i < 0 ? i + n : i); }
 
+// cv2.projectPoints of one point, no distortion (cvProjectPoints2Internal
+// order; the device project() in mvs_kernels.hip is the same expression)
+void project_host(const double* K, const double* Rp, const double* t, const double* M, double* out) {
+    double x = Rp[0] * M[0] + Rp[1] * M[1] + Rp[2] * M[2] + t[0];
+    double y = Rp[3] * M[0] + Rp[4] * M[1] + Rp[5] * M[2] + t[1];
+    double z = Rp[6] * M[0] + Rp[7] * M[1] + Rp[8] * M[2] + t[2];
+    z = z != 0.0 ? 1.0 / z : 1.0;
+    x *= z;
+    y *= z;
+    out[0] = x * K[0] + K[2];
+    out[1] = y * K[4] + K[5];
+}
+
+// getProjectionMatrix(K, R, t) = K @ [R | t] (utils.py:234-236) as OpenBLAS
+// evaluates the 3x3 by 3x4 product: an FMA chain per entry
+void projection_matrix(const double* K, const double* R, const double* t, double* P) {
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 4; c++) {
+            const double e0 = c < 3 ? R[c] : t[0], e1 = c < 3 ? R[3 + c] : t[1],
+                         e2 = c < 3 ? R[6 + c] : t[2];
+            P[4 * r + c] = fma_dot3(K[3 * r], K[3 * r + 1], K[3 * r + 2], e0, e1, e2);
+        }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -283,6 +307,10 @@ struct mvs_ctx {
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand, t_pcnt;
     DevBuf<double> t_psum;
+    // SfM front-end scratch (Harris maps, descriptors, match rows)
+    DevBuf<float> f_resp, f_dil;
+    DevBuf<uint32_t> f_key, f_desc;
+    DevBuf<int32_t> f_rows, f_pts, f_mom, f_best;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
     int variant = 0;       // tiled-kernel variant (env MVS_VARIANT), see mvs_kernels.hip
     int chunk3 = 256;      // candidates per work item of the v3 tiled kernel (env MVS_TILE_CHUNK)
@@ -1270,6 +1298,138 @@ int mvs_rodrigues_roundtrip(const double* R, double* Rp) {
 int mvs_triangulate(const double* P1, const double* P2, const double* x1, const double* x2, double* X4) {
     if (!P1 || !P2 || !x1 || !x2 || !X4) return MVS_E_ARG;
     triangulate(P1, P2, x1, x2, X4);
+    return 0;
+}
+
+// ---- SfM front-end (HarrisFeatures.py, SFM.py) ----
+
+int mvs_harris_points(mvs_ctx* ctx, int view, int32_t* out, int64_t cap, int64_t* n_out) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    return guarded(ctx, [&]() -> int {
+        if (!n_out || (cap > 0 && !out)) throw Fail{MVS_E_ARG, "null output"};
+        if (view < 0 || view >= ctx->V) throw Fail{MVS_E_ARG, "view out of range"};
+        const int64_t npx = (int64_t)ctx->H * ctx->W;
+        ctx->f_resp.ensure(npx);
+        ctx->f_dil.ensure(npx);
+        ctx->f_key.ensure(1);
+        ctx->f_rows.ensure(2 * (size_t)ctx->H + 1);
+        hipStream_t s = ctx->stream;
+        int32_t* rowcnt = ctx->f_rows.p;
+        int32_t* rowoff = ctx->f_rows.p + ctx->H;
+        if (mvs_launch_harris(&ctx->sc, view, 0.04, ctx->f_resp.p, ctx->f_dil.p, ctx->f_key.p, rowcnt,
+                              rowoff, s) != 0)
+            throw Fail{MVS_E_HIP, "harris launch failed"};
+        int32_t total = 0;
+        HIPCHK(hipMemcpyAsync(&total, rowoff + ctx->H, sizeof total, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        *n_out = total;
+        const int64_t m = std::min<int64_t>(total, cap);
+        if (m > 0) {
+            ctx->f_pts.ensure(2 * (size_t)total);
+            if (mvs_launch_harris_write(&ctx->sc, ctx->f_dil.p, ctx->f_key.p, rowoff, ctx->f_pts.p, total,
+                                        s) != 0)
+                throw Fail{MVS_E_HIP, "harris write launch failed"};
+            HIPCHK(hipMemcpyAsync(out, ctx->f_pts.p, 2 * m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        return 0;
+    });
+}
+
+int mvs_match_two_sided(mvs_ctx* ctx, int view_a, const int32_t* pts_a, int64_t n_a, int view_b,
+                        const int32_t* pts_b, int64_t n_b, int wid, double thr, int32_t* m12,
+                        int32_t* best12, int32_t* best21) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    return guarded(ctx, [&]() -> int {
+        if (n_a < 0 || n_b < 0 || (n_a && (!pts_a || !m12)) || (n_b && !pts_b))
+            throw Fail{MVS_E_ARG, "bad point arrays"};
+        if (view_a < 0 || view_a >= ctx->V || view_b < 0 || view_b >= ctx->V)
+            throw Fail{MVS_E_ARG, "view out of range"};
+        if (wid < 1 || (2 * wid + 1) * (2 * wid + 1) > 128) throw Fail{MVS_E_UNSUPPORTED, "wid must be 1..5"};
+        // getDescFeatures keeps only windows inside these bounds (HarrisFeatures.py:128)
+        for (int side = 0; side < 2; ++side) {
+            const int32_t* p = side ? pts_b : pts_a;
+            const int64_t n = side ? n_b : n_a;
+            for (int64_t i = 0; i < n; ++i) {
+                const int r = p[2 * i], c = p[2 * i + 1];
+                if (!(r - wid >= 0 && r + wid + 1 < ctx->H && c - wid > 0 && c + wid + 1 < ctx->W))
+                    throw Fail{MVS_E_ARG, "point outside getDescFeatures' bounds"};
+            }
+        }
+        if (n_a == 0) return 0;
+        const int npx = (2 * wid + 1) * (2 * wid + 1);
+        constexpr int DW = 32;   // descriptor dwords (kDescWords)
+        const int64_t n = n_a + n_b;
+        ctx->f_pts.ensure(2 * (size_t)n);
+        ctx->f_desc.ensure((size_t)DW * n + 4);
+        ctx->f_mom.ensure(2 * (size_t)n);
+        ctx->f_best.ensure((size_t)n);
+        hipStream_t s = ctx->stream;
+        HIPCHK(hipMemcpyAsync(ctx->f_pts.p, pts_a, 2 * n_a * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        if (n_b)
+            HIPCHK(hipMemcpyAsync(ctx->f_pts.p + 2 * n_a, pts_b, 2 * n_b * sizeof(int32_t),
+                                  hipMemcpyHostToDevice, s));
+        uint32_t* dA = ctx->f_desc.p;
+        uint32_t* dB = ctx->f_desc.p + (size_t)DW * n_a;
+        int32_t* S = ctx->f_mom.p;
+        int32_t* SS = ctx->f_mom.p + n;
+        if (mvs_launch_gather_desc(&ctx->sc, view_a, ctx->f_pts.p, n_a, wid, dA, S, SS, s) != 0 ||
+            mvs_launch_gather_desc(&ctx->sc, view_b, ctx->f_pts.p + 2 * n_a, n_b, wid, dB, S + n_a,
+                                   SS + n_a, s) != 0)
+            throw Fail{MVS_E_HIP, "descriptor launch failed"};
+        int32_t* b12 = ctx->f_best.p;
+        int32_t* b21 = ctx->f_best.p + n_a;
+        if (mvs_launch_match_rows(dA, S, SS, n_a, dB, S + n_a, SS + n_a, n_b, npx, thr, b12, s) != 0 ||
+            mvs_launch_match_rows(dB, S + n_a, SS + n_a, n_b, dA, S, SS, n_a, npx, thr, b21, s) != 0)
+            throw Fail{MVS_E_HIP, "match launch failed"};
+        std::vector<int32_t> h12(n_a), h21(n_b);
+        HIPCHK(hipMemcpyAsync(h12.data(), b12, n_a * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        if (n_b) HIPCHK(hipMemcpyAsync(h21.data(), b21, n_b * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        // MatchTwoSided's symmetric check (HarrisFeatures.py:60-64)
+        for (int64_t i = 0; i < n_a; ++i) {
+            const int32_t j = h12[i];
+            m12[i] = (j >= 0 && h21[j] == (int32_t)i) ? j : -1;
+        }
+        if (best12) std::copy(h12.begin(), h12.end(), best12);
+        if (best21) std::copy(h21.begin(), h21.end(), best21);
+        return 0;
+    });
+}
+
+int mvs_sfm_pair(const double* KA, const double* RA, const double* tA, const double* KB,
+                 const double* RB, const double* tB, int64_t n, const float* q, const float* tr,
+                 double max_err, float* pt, uint8_t* keep) {
+    if (!KA || !RA || !tA || !KB || !RB || !tB || n < 0 || (n && (!q || !tr || !pt || !keep)))
+        return set_err(nullptr, Fail{MVS_E_ARG, "null argument"});
+    double P1[12], P2[12], RpA[9], RpB[9];
+    projection_matrix(KA, RA, tA, P1);
+    projection_matrix(KB, RB, tB, P2);
+    rodrigues_roundtrip(RA, RpA);
+    rodrigues_roundtrip(RB, RpB);
+    for (int64_t i = 0; i < n; ++i) {
+        // cv2.triangulatePoints on float32 points: double DLT, float32 result
+        const double x1[2] = {q[2 * i], q[2 * i + 1]}, x2[2] = {tr[2 * i], tr[2 * i + 1]};
+        double X4[4];
+        triangulate(P1, P2, x1, x2, X4);
+        const float w = (float)X4[3];
+        keep[i] = 0;
+        pt[3 * i] = pt[3 * i + 1] = pt[3 * i + 2] = 0.f;
+        if (w == 0.f) continue;                    // SFM.py:69-72: not added
+        float p[3];
+        for (int k = 0; k < 3; ++k) p[k] = (float)X4[k] / w;
+        for (int k = 0; k < 3; ++k) pt[3 * i + k] = p[k];
+        // projectPoint on the float32 point: double projection, float32 result;
+        // np.linalg.norm of the float32 residual (SFM.py:75-78)
+        const double M[3] = {p[0], p[1], p[2]};
+        double oa[2], ob[2];
+        project_host(KA, RpA, tA, M, oa);
+        project_host(KB, RpB, tB, M, ob);
+        const float ra0 = (float)oa[0] - q[2 * i], ra1 = (float)oa[1] - q[2 * i + 1];
+        const float rb0 = (float)ob[0] - tr[2 * i], rb1 = (float)ob[1] - tr[2 * i + 1];
+        const float ea = std::sqrt(ra0 * ra0 + ra1 * ra1), eb = std::sqrt(rb0 * rb0 + rb1 * rb1);
+        keep[i] = ((double)ea > max_err || (double)eb > max_err) ? 0 : 1;
+    }
     return 0;
 }
 

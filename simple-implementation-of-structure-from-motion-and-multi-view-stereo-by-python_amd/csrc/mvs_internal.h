@@ -141,6 +141,17 @@ int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledAr
                            int variant, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, int wid,
                       hipStream_t s);
+// SfM front-end (HarrisFeatures.py): Harris response + dilate + global max +
+// per-row counts and offsets (rowoff[H] = total), then the [col, row] write
+int mvs_launch_harris(const SceneDev* sc, int v, double k, float* resp, float* dil, uint32_t* maxkey,
+                      int32_t* rowcnt, int32_t* rowoff, hipStream_t s);
+int mvs_launch_harris_write(const SceneDev* sc, const float* dil, const uint32_t* maxkey,
+                            const int32_t* rowoff, int32_t* out, int64_t cap, hipStream_t s);
+int mvs_launch_gather_desc(const SceneDev* sc, int v, const int32_t* rc, int64_t n, int wid,
+                           uint32_t* desc, int32_t* S, int32_t* SS, hipStream_t s);
+int mvs_launch_match_rows(const uint32_t* dA, const int32_t* SA, const int32_t* SSA, int64_t nA,
+                          const uint32_t* dB, const int32_t* SB, const int32_t* SSB, int64_t nB,
+                          int npx, double thr, int32_t* best, hipStream_t s);
 // Packed record rows for the multi-GPU stage exchange: int64 words
 // [c0 c1 c2 n0 n1 n2 x y | mask[words] | R + count<<32 | cell0 + cell1<<32 | rgba + accept<<32]
 int mvs_launch_pack_records(RecordsDev rec, int words, int64_t first, int64_t n, int64_t* out,
