@@ -39,7 +39,7 @@ def main(args, threshold=0.01, MIN_REPROJECTION_ERROR=0.3):
         if not dist.is_initialized():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     imgs = mvs.read_imgs(args)
-    if args.seeds:
+    if getattr(args, "seeds", None):
         global_set = mvs.SeedSet.load(args.seeds)
     else:
         # SfM.StructureFromMotion (main.py:28) with the Harris/NCC front-end on
@@ -49,11 +49,11 @@ def main(args, threshold=0.01, MIN_REPROJECTION_ERROR=0.3):
         n_obs, n_pts, _ = global_set.getInfo()
         print(f"SfM: {st['pairs']} pairs, {st['correspondences']} correspondences, "
               f"{st['kept']} triangulated, {n_pts} tracks / {n_obs} observations")
-    if args.save_tracks and (world == 1 or int(os.environ.get("RANK", "0")) == 0):
+    if getattr(args, "save_tracks", None) and (world == 1 or int(os.environ.get("RANK", "0")) == 0):
         import numpy as np
         off, view, xy = mvs.utils.tracks_to_arrays(global_set.getInfo()[2])
         np.savez(args.save_tracks, track_off=off, obs_view=view, obs_xy=xy)
-    mvs.DensePointsWithMVS2(imgs, global_set, args, max_pops=args.max_pops)
+    mvs.DensePointsWithMVS2(imgs, global_set, args, max_pops=getattr(args, "max_pops", 100000))
     st = mvs.MVS2.last_stats
     if world == 1 or int(os.environ.get("RANK", "0")) == 0:
         print("pops {pops} tests {tests} accepted {accepts} gpu-scored {scored} sweeps {sweeps}".format(**st))
