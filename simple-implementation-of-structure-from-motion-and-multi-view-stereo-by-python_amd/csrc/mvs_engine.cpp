@@ -15,6 +15,7 @@
 // Compiled with -ffp-contract=off: host geometry (Jacobi SVD, triangulation,
 // camera constants) follows OpenCV's / numpy's operation order.
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -703,7 +704,14 @@ struct Engine {
     // fetch_sweep() brings the sweep's gates to the host for the next plan().
     // Every rank runs the same plan() on the same records, so all commits
     // agree.
-    std::vector<int32_t> queue;
+    // the FIFO, run-length encoded: an accepted patch is enqueued |V| times in
+    // a row (MVS2.py:376-379), stored once with its copy count
+    struct QEntry {
+        int32_t rec;
+        int32_t left;
+    };
+    std::vector<QEntry> queue;
+    int64_t queued = 0;              // copies still in the FIFO
     size_t qhead = 0;
     std::vector<int32_t> unscored;   // records in order of first enqueue
     size_t ucur = 0;
@@ -715,13 +723,15 @@ struct Engine {
     void expand_init() {
         trace = std::getenv("MVS_TRACE") != nullptr;
         queue.clear();
-        queue.reserve(1 << 20);
+        queue.reserve(1 << 18);
+        queued = 0;
         qhead = 0;
         unscored.clear();
         ucur = 0;
         pops = 0;
         for (int64_t r = 0; r < n_seeds; ++r) {
-            queue.push_back((int32_t)r);
+            queue.push_back(QEntry{(int32_t)r, 1});
+            ++queued;
             unscored.push_back((int32_t)r);
             h_enq[r] = 1;
         }
@@ -731,10 +741,11 @@ struct Engine {
     int64_t plan() {
         // ordered commit until the FIFO head has no scored children
         while (qhead < queue.size() && pops < max_pops) {
-            const int32_t r = queue[qhead];
+            const int32_t r = queue[qhead].rec;
             const int64_t base = h_child[r];
             if (base < 0) break;
-            ++qhead;
+            if (--queue[qhead].left == 0) ++qhead;
+            --queued;
             ++pops;
             const long ci = h_cell[2 * r], cj = h_cell[2 * r + 1];
             int h = 0;
@@ -753,7 +764,10 @@ struct Engine {
                             if (h_accept[child]) {
                                 fill_record(child);
                                 events.push_back((int32_t)child);
-                                for (int k = 0; k < h_count[child]; ++k) queue.push_back((int32_t)child);
+                                if (h_count[child] > 0) {
+                                    queue.push_back(QEntry{(int32_t)child, h_count[child]});
+                                    queued += h_count[child];
+                                }
                                 if (!h_enq[child]) {
                                     h_enq[child] = 1;
                                     unscored.push_back((int32_t)child);
@@ -768,7 +782,7 @@ struct Engine {
         }
         if (qhead >= queue.size() || pops >= max_pops) {
             stat_pops = pops;
-            stat_queue_left = (int64_t)(queue.size() - qhead);
+            stat_queue_left = queued;
             sweep_n = 0;
             return 0;
         }
@@ -820,11 +834,26 @@ struct Engine {
 
     void fetch_sweep() { fetch_range(sweep_first, sweep_n); }
 
+    // host time per phase (seconds), printed by mvs_stage_run under MVS_STAGE_TIMES
+    double t_plan = 0, t_score = 0, t_fetch = 0;
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+
     void expand() {
         expand_init();
-        while (plan() > 0) {
+        for (;;) {
+            double t0 = now();
+            const int64_t nj = plan();
+            double t1 = now();
+            t_plan += t1 - t0;
+            if (nj == 0) break;
             score_range(0, sweep_n);
+            HIPCHK(hipStreamSynchronize(s));
+            double t2 = now();
+            t_score += t2 - t1;
             fetch_sweep();
+            t_fetch += now() - t2;
         }
     }
 
@@ -840,7 +869,10 @@ struct Engine {
     // lexicographic, append order within a key, first sight of each object.  A
     // patch is appended under (u, cell) for every u in its V list, so its first
     // sight is at (min u, cell), in fill order among equal keys.
+    double t_out[5] = {0, 0, 0, 0, 0};   // copy-back, keys, sort, rows, end stamp (MVS_STAGE_TIMES)
+
     void output(mvs_stage_result* res) {
+        double ta = now();
         std::vector<double> hc(nrec * 3);
         std::vector<uint8_t> hcol(nrec * 4);
         if (nrec) {
@@ -848,12 +880,16 @@ struct Engine {
             HIPCHK(hipMemcpyAsync(hcol.data(), d_color.p, nrec * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
+        double tb = now();
+        t_out[0] = tb - ta;
         auto row = [&](std::vector<double>& out, int64_t r) {
             out.push_back(hc[3 * r]); out.push_back(hc[3 * r + 1]); out.push_back(hc[3 * r + 2]);
             out.push_back(hcol[4 * r]); out.push_back(hcol[4 * r + 1]); out.push_back(hcol[4 * r + 2]);
         };
         for (int64_t r = 0; r < n_seeds; ++r) row(res->initial, r);
-        std::vector<std::pair<int64_t, int64_t>> keyed;   // (key, event index)
+        // stable sort of the events by key (min view, cell x, cell y): LSD radix
+        // sort, 11 bits per pass (the key space is V * nci * ncj)
+        std::vector<uint64_t> keyed, tmp;   // key << 32 | event index
         keyed.reserve(events.size());
         for (size_t e = 0; e < events.size(); ++e) {
             const int64_t r = events[e];
@@ -862,11 +898,24 @@ struct Engine {
                 if (h_mask[r * words + w]) minv = 64 * w + __builtin_ctzll(h_mask[r * words + w]);
             const int cx = h_cell[2 * r], cy = h_cell[2 * r + 1];
             if (minv < 0 || cx < 0 || cx >= nci || cy < 0 || cy >= ncj) continue;
-            keyed.emplace_back(((int64_t)minv * nci + cx) * ncj + cy, (int64_t)e);
+            keyed.push_back(((uint64_t)(((int64_t)minv * nci + cx) * ncj + cy) << 32) | (uint64_t)e);
         }
-        std::sort(keyed.begin(), keyed.end());
+        const uint64_t kmax = (uint64_t)V * nci * ncj;
+        double tc = now();
+        t_out[1] = tc - tb;
+        tmp.resize(keyed.size());
+        for (int shift = 32; shift < 64 && (kmax >> (shift - 32)) > 0; shift += 11) {
+            size_t cnt[2049] = {0};
+            for (uint64_t k : keyed) ++cnt[((k >> shift) & 2047) + 1];
+            for (int b = 0; b < 2048; ++b) cnt[b + 1] += cnt[b];
+            for (uint64_t k : keyed) tmp[cnt[(k >> shift) & 2047]++] = k;
+            keyed.swap(tmp);
+        }
+        double td = now();
+        t_out[2] = td - tc;
         res->all.reserve(keyed.size() * 6);
-        for (auto& k : keyed) row(res->all, events[k.second]);
+        for (uint64_t k : keyed) row(res->all, events[(uint32_t)k]);
+        t_out[3] = now() - td;
         res->stats[0] = stat_pops;
         res->stats[1] = stat_tests;
         res->stats[2] = (int64_t)events.size();
@@ -906,10 +955,14 @@ Engine* make_engine(mvs_ctx* ctx, int cell_size, double scale, int wid, int64_t 
 }
 
 void finish_engine(mvs_ctx* ctx, Engine* E, mvs_stage_result* res) {
-    E->output(res);
+    // the exact-path counter first: a device-to-host copy issued after
+    // output() has written ~35 MB of fresh host memory took ~25 ms here
     int32_t h = 0;
     HIPCHK(hipMemcpyAsync(&h, ctx->d_exact.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    const double t = Engine::now();
+    E->output(res);
+    E->t_out[4] = Engine::now() - t;
     res->stats[7] = h;
 }
 }  // namespace
@@ -1095,10 +1148,26 @@ int mvs_stage_run(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off, cons
         std::unique_ptr<mvs_stage_result> res(new mvs_stage_result());
         std::unique_ptr<Engine> E(make_engine(ctx, cell_size, scale, wid, max_pops));
         HIPCHK(hipMemsetAsync(ctx->d_exact.p, 0, sizeof(int32_t), ctx->stream));
+        const double t0 = Engine::now();
         E->seed(n_tracks, track_off, obs_view, obs_xy);
+        const double t1 = Engine::now();
         E->expand();
+        const double t2 = Engine::now();
         finish_engine(ctx, E.get(), res.get());
+        const double t3 = Engine::now();
+        if (std::getenv("MVS_STAGE_TIMES"))
+            std::fprintf(stderr, "stage times: seed %.4f s, expand %.4f s (commit/plan %.4f, GPU sweeps %.4f, "
+                                 "fetch %.4f), output %.4f s\n",
+                         t1 - t0, t2 - t1, E->t_plan, E->t_score, E->t_fetch, t3 - t2);
+        if (std::getenv("MVS_STAGE_TIMES"))
+            std::fprintf(stderr, "  output: copy-back %.4f, keys %.4f, sort %.4f, rows %.4f s; output() %.4f s\n",
+                         E->t_out[0], E->t_out[1], E->t_out[2], E->t_out[3], E->t_out[4]);
         *out = res.release();
+        if (std::getenv("MVS_STAGE_TIMES")) {
+            const double td = Engine::now();
+            E.reset();
+            std::fprintf(stderr, "  engine teardown %.4f s\n", Engine::now() - td);
+        }
         return 0;
     });
 }

@@ -264,6 +264,58 @@ def test_stage_empty_and_ragged_tracks(ctx, oracle_scene, seeds):
     assert np.array_equal(allp, oall)
 
 
+def _smooth_ring(pkg, V, H=96, W=128):
+    rgb, K, R, t = pkg.synthetic.ring_scene(V=V, H=H, W=W, seed=V)
+    # smooth the textures so that some views pass
+    rgb = ((rgb.astype(np.uint16) + np.roll(rgb, 1, axis=0)) // 2).astype(np.uint8)
+    return rgb, K, R, t
+
+
+@pytest.mark.parametrize("V,wid", [(68, 5), (100, 3), (256, 3)])
+def test_view_groups_wid_and_partial_group(pkg, orc, V, wid):
+    """k_score_tiledg with a 4-view last group (V = 68) and at wid 3."""
+    H, W = 96, 128
+    rgb, K, R, t = _smooth_ring(pkg, V, H, W)
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        sc = orc.Scene(rgb, K, R, t)
+        c, ref = pkg.synthetic.candidates(3000, K, R, t, W=W, H=H, seed=2)
+        for thr in (0.2, 0.6):
+            got = cx.score(c, ref, thr, wid)
+            exp = sc.score_batch(c, ref, thr, wid)
+            for g, e in zip(got[:3], exp[:3]):
+                assert np.array_equal(g, e)
+            np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+
+
+def test_view_groups_threshold_on_reference_value(pkg, orc):
+    """V > 64: thresholds exactly on a reference ctNcc value route lanes through
+    the guard band to k_score_fix's NS-slot re-score (numpy-order ctNcc)."""
+    H, W = 96, 128
+    rgb, K, R, t = _smooth_ring(pkg, 100, H, W)
+    c, ref = pkg.synthetic.candidates(200, K, R, t, W=W, H=H, seed=4)
+    sc = orc.Scene(rgb, K, R, t)
+    checked = 0
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        hits0 = cx.exact_hits()
+        for i in range(len(ref)):
+            ncc = sc.photo_ncc(c[i], ref[i], 5)
+            fin = np.nonzero(np.isfinite(ncc) & (ncc > 0.05))[0]
+            if len(fin) == 0:
+                continue
+            v = fin[-1]                                  # a view in the last group when possible
+            for thr in (ncc[v], np.nextafter(ncc[v], 2.0), np.nextafter(ncc[v], -2.0)):
+                cc, rr = np.tile(c[i], (3000, 1)), np.full(3000, ref[i], np.int32)
+                got = cx.score(cc, rr, float(thr), 5)
+                exp = sc.score_batch(cc[:1], rr[:1], float(thr), 5)
+                assert np.array_equal(got[1][:1], exp[1]) and np.array_equal(got[2][:1], exp[2])
+                assert (got[1] == got[1][0]).all()
+            checked += 1
+            if checked >= 6:
+                break
+        assert checked >= 3
+        assert cx.exact_hits() > hits0
+
+
 @pytest.mark.parametrize("V", [5, 100, 102, 192, 256])
 def test_view_count_variants(pkg, orc, V):
     """Lane-slot layouts: V < 64, one extra slot, and the 4-slot 256-view case;
