@@ -483,3 +483,43 @@ def test_one_hip_runtime_whatever_the_import_order(tmp_path):
         "ctx.close(); print('ok')\n")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("wid", [5, 3])
+def test_bench_sweep_full_size(ctx, oracle_scene, dino, wid):
+    """The bench's own workload at its full size (2^20 candidates, seed 0,
+    MIN_NCC 0.7, dinoRing): every output against the oracle on all host cores,
+    plus the size-independent invariants of the photo test."""
+    import os
+    rgb, K, R, t = dino
+    n = 1 << 20
+    c, ref = bench_candidates(n, K, R, t, seed=0)
+    xy, mask, count, avg = ctx.score(c, ref, 0.7, wid)
+    m = mask.reshape(n).astype(np.uint64)
+    pop = np.array([bin(int(v)).count("1") for v in m[:20000]])
+    assert np.array_equal(pop, count[:20000])                          # |V| = popcount
+    assert not ((m >> ref.astype(np.uint64)) & np.uint64(1)).any()    # R never in its own V
+    assert (avg[count == 0] == 0).all() and (avg[count > 0] > 0.7).all()
+    oxy, omask, ocount, oavg = oracle_scene.score_batch(c, ref, 0.7, wid,
+                                                        nthreads=min(os.cpu_count() or 1, 16))
+    assert np.array_equal(xy, oxy)
+    assert np.array_equal(mask, omask)
+    assert np.array_equal(count, ocount)
+    np.testing.assert_allclose(avg, oavg, rtol=0, atol=AVG_TOL)
+
+
+def test_ring256_quarter_sweep(pkg, orc):
+    """SURVEY 8(d) config 4 scene (256 views, 1920x1080, uniform-random texture)
+    with a quarter of the bench sweep (2^18 candidates) on the view-group
+    scorer, against the oracle."""
+    import os
+    syn = pkg.synthetic
+    rgb, K, R, t = syn.ring_scene(256, 1080, 1920, seed=0)
+    c, ref = syn.candidates(1 << 18, K, R, t, W=1920, H=1080, seed=0)
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        got = cx.score(c, ref, 0.7, 5)
+    sc = orc.Scene(rgb, K, R, t)
+    exp = sc.score_batch(c, ref, 0.7, 5, nthreads=min(os.cpu_count() or 1, 16))
+    for g, e in zip(got[:3], exp[:3]):
+        assert np.array_equal(g, e)
+    np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
