@@ -2525,13 +2525,19 @@ constexpr int kDescWords = 32;
 __global__ void k_gather_desc(const SceneDev sc, int v, const int32_t* __restrict__ rc, int64_t n,
                               int wid, uint32_t* __restrict__ desc, int32_t* __restrict__ S,
                               int32_t* __restrict__ SS) {
+    // one lane per (point, descriptor dword): 32 lanes per point, the moments
+    // reduced across those lanes
     const int nb = 2 * wid + 1, npx = nb * nb;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int r = rc[2 * i], q = rc[2 * i + 1];
+    const int64_t total = n * kDescWords;
+    for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < ((total + 63) & ~(int64_t)63);
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = id / kDescWords;
+        const int k = (int)(id % kDescWords);
+        uint32_t wd = 0;
         int32_t s = 0, ss = 0;
-        for (int k = 0; k < kDescWords; ++k) {
-            uint32_t wd = 0;
+        if (i < n) {
+            const int r = rc[2 * i], q = rc[2 * i + 1];
+#pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const int p = 4 * k + b;
                 if (p < npx) {
@@ -2541,10 +2547,17 @@ __global__ void k_gather_desc(const SceneDev sc, int v, const int32_t* __restric
                     ss += (int32_t)(g * g);
                 }
             }
-            desc[i * kDescWords + k] = wd;
+            desc[id] = wd;
         }
-        S[i] = s;
-        SS[i] = ss;
+#pragma unroll
+        for (int off = kDescWords / 2; off > 0; off >>= 1) {
+            s += __shfl_xor(s, off, kDescWords);
+            ss += __shfl_xor(ss, off, kDescWords);
+        }
+        if (i < n && k == 0) {
+            S[i] = s;
+            SS[i] = ss;
+        }
     }
 }
 
@@ -2658,7 +2671,7 @@ extern "C" int mvs_launch_gather_desc(const SceneDev* sc, int v, const int32_t* 
                                       uint32_t* desc, int32_t* S, int32_t* SS, hipStream_t s) {
     if (n == 0) return 0;
     if (wid < 1 || (2 * wid + 1) * (2 * wid + 1) > 4 * kDescWords) return -2;
-    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    const int blocks = (int)std::min<int64_t>((n * kDescWords + 255) / 256, 4096);
     hipLaunchKernelGGL(k_gather_desc, dim3(blocks), dim3(256), 0, s, *sc, v, rc, n, wid, desc, S, SS);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
