@@ -120,7 +120,7 @@ def main():
         if world > 1:
             # the sweep's exchange (parallel.py): every rank's accepted set
             # (accept bitmap + V masks; count = popcount, centroids known) to every rank
-            blocks = par.all_gather_compact(par.pack_compact(count, mask, vlb))
+            blocks = par.exchange_accepted(count, mask, vlb)
             gathered["n"] = sum((b.numel() - 1 - (n + 63) // 64) // words for b in blocks)
 
     def timed(wid, steps, warmup):

@@ -112,6 +112,44 @@ def all_gather_compact(block, group=None):
     return [flat[r * kmax: r * kmax + sizes[r]] for r in range(world)]
 
 
+def exchange_accepted(count, mask, vlb, group=None):
+    """pack_compact + all_gather_compact with ONE host synchronisation: the
+    accepted counts travel first (a tiny all-gather), their host copy sizes
+    both the static-size compaction (nonzero_static, no sync of its own) and
+    the padded data all-gather.  Returns the ranks' compact blocks."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    n = count.numel()
+    words = mask.shape[1]
+    nbw = (n + 63) // 64
+    acc = count >= vlb
+    k = acc.sum().to(torch.int64).reshape(1)
+    if world > 1:
+        ks = torch.empty(world, dtype=torch.int64, device=count.device)
+        dist.all_gather_into_tensor(ks, k, group=group)
+    else:
+        ks = k
+    a = acc.to(torch.int64)
+    if nbw * 64 != n:
+        a = torch.cat([a, a.new_zeros(nbw * 64 - n)])
+    sh = torch.arange(64, dtype=torch.int64, device=count.device)
+    bits = (a.view(nbw, 64) << sh).sum(1)
+    sizes = ks.tolist()                               # the one host sync
+    rank = dist.get_rank(group) if world > 1 else 0
+    kmax = max(sizes)
+    buf = torch.zeros(1 + nbw + kmax * words, dtype=torch.int64, device=count.device)
+    buf[0] = k[0]
+    buf[1:1 + nbw] = bits
+    if sizes[rank]:
+        idx = torch.nonzero_static(acc, size=sizes[rank]).squeeze(1)
+        buf[1 + nbw:1 + nbw + sizes[rank] * words] = mask[idx].reshape(-1).view(torch.int64)
+    if world == 1:
+        return [buf[:1 + nbw + sizes[0] * words]]
+    flat = torch.empty(world * buf.numel(), dtype=torch.int64, device=count.device)
+    dist.all_gather_into_tensor(flat, buf, group=group)
+    L = buf.numel()
+    return [flat[r * L: r * L + 1 + nbw + sizes[r] * words] for r in range(world)]
+
+
 _POP8 = None
 
 

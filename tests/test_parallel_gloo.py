@@ -177,6 +177,11 @@ def _compact_worker(rank, world, port, n, words, out_dir):
     blk = par.pack_compact(torch.from_numpy(cnt), torch.from_numpy(mask), 3)
     blocks = par.all_gather_compact(blk)
     idx, count, m = par.unpack_compact(blocks, n, words)
+    # the single-sync form the bench uses delivers the same blocks
+    blocks2 = par.exchange_accepted(torch.from_numpy(cnt), torch.from_numpy(mask), 3)
+    assert len(blocks2) == len(blocks)
+    for b1, b2 in zip(blocks, blocks2):
+        assert torch.equal(b1, b2)
     np.savez(os.path.join(out_dir, f"c{rank}.npz"), idx=idx.numpy(), count=count.numpy(),
              mask=m.numpy())
     dist.barrier()
