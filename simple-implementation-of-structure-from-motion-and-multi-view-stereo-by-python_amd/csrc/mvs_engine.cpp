@@ -315,6 +315,7 @@ struct mvs_ctx {
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
     int variant = 0;       // tiled-kernel variant (env MVS_VARIANT), see mvs_kernels.hip
     int chunk3 = 256;      // candidates per work item of the v3 tiled kernel (env MVS_TILE_CHUNK)
+    int tiles_clean_ntiles = -1;   // tile counters known zero for this tile count (-1: unknown)
     // kernel timing (mvs_kernel_timing): one event pair per scoring launch
     bool timing = false;
     std::vector<hipEvent_t> ev;
@@ -428,7 +429,9 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         TiledArgs t{};
         mvs_tiled_geometry(ctx->W, ctx->H, mfma ? 1 : 0, &t.tw, &t.th, &t.ntx, &t.nty);
         const int ntiles = t.ntx * t.nty;
+        const int32_t* tiles_before = ctx->t_tiles.p;
         ctx->t_tiles.ensure((size_t)3 * (ntiles + 2) + 8);
+        if (ctx->t_tiles.p != tiles_before) ctx->tiles_clean_ntiles = -1;
         const int groups = grouped ? (ctx->V + 63) / 64 : 1;
         ctx->t_cand.ensure((size_t)(5 + groups) * n);   // fix_list: one entry per (candidate, group)
         t.ntiles = ntiles;
@@ -450,10 +453,13 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.sorted = (int2*)(ctx->t_cand.p + 3 * n);
         t.fix_list = ctx->t_cand.p + 5 * n;
         t.xq = ctx->t_tiles.p + 3 * (ntiles + 2);
+        t.zero_first = ctx->tiles_clean_ntiles != ntiles ? 1 : 0;
+        ctx->tiles_clean_ntiles = -1;            // dirty until the sequence is queued
         hipEvent_t e0, e1;
         ctx->next_events(&e0, &e1);
         if (mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, variant, s, e0, e1) != 0)
             throw Fail{MVS_E_HIP, "tiled score launch failed"};
+        ctx->tiles_clean_ntiles = ntiles;        // k_tile_scan leaves the counters zero
         return;
     }
     hipEvent_t e0, e1;

@@ -91,6 +91,11 @@ struct TiledArgs {
     int32_t* part_cnt;         // n*groups
     double* part_sum;          // n*groups
     int32_t* xq;               // 8 work-queue heads, one per XCD label (blockIdx % 8)
+    // k_tile_scan leaves every counter zero for the next batch (it zeroes the
+    // bin counts after reading them and the queue heads / fix_count before the
+    // scorer uses them); zero_first = 1 asks the launcher to clear them first
+    // (new scratch, or a previous sequence that did not complete)
+    int zero_first;
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).

@@ -597,11 +597,18 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
         const int c = t.tile_count[k];
         rc += c;
         ri += (c + t.chunk - 1) / t.chunk;
+        t.tile_count[k] = 0;          // clean for the next batch's k_bin
     }
     if (tid == 1023) {
         t.tile_off[t.ntiles] = part_c[1023];
         t.item_off[t.ntiles] = part_i[1023];
     }
+    // work-queue heads and the fix-list length start this batch at zero
+    if (tid == 0) {
+        t.tile_count[t.ntiles] = 0;
+        t.tile_count[t.ntiles + 1] = 0;
+    }
+    if (t.xq && tid < 8) t.xq[tid] = 0;
 }
 
 __global__ void k_scatter(const ScoreArgs a, const TiledArgs t) {
@@ -2087,8 +2094,11 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
                          hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     using G = TileGeom<WID>;
     if (a->n == 0) return 0;
-    // tile counters, the work-queue head (tile_count[ntiles]) and fix_count
-    if (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess) return -1;
+    // tile counters, the work-queue head (tile_count[ntiles]) and fix_count:
+    // left at zero by the previous batch's k_tile_scan unless zero_first
+    if (t->zero_first &&
+        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess)
+        return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);
     hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
@@ -2169,8 +2179,10 @@ int launch_score_tiledg_w(const SceneDev* sc, const ScoreArgs* a, const TiledArg
         t->tw != kTW || t->th != kTH)
         return -3;
     if (t->xq == nullptr) return -3;
-    if (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess) return -1;
-    if (hipMemsetAsync(t->xq, 0, sizeof(int32_t) * 8, s) != hipSuccess) return -1;
+    if (t->zero_first &&
+        (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess ||
+         hipMemsetAsync(t->xq, 0, sizeof(int32_t) * 8, s) != hipSuccess))
+        return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);
     hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
