@@ -307,6 +307,7 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand, t_pcnt;
+    DevBuf<int2> t_items;
     DevBuf<double> t_psum;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
     DevBuf<float> f_resp, f_dil;
@@ -453,6 +454,9 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.sorted = (int2*)(ctx->t_cand.p + 3 * n);
         t.fix_list = ctx->t_cand.p + 5 * n;
         t.xq = ctx->t_tiles.p + 3 * (ntiles + 2);
+        // at most one partial chunk per tile beyond the full ones
+        ctx->t_items.ensure((size_t)(n / std::max(t.chunk, 1) + ntiles + 2));
+        t.items = ctx->t_items.p;
         t.zero_first = ctx->tiles_clean_ntiles != ntiles ? 1 : 0;
         ctx->tiles_clean_ntiles = -1;            // dirty until the sequence is queued
         hipEvent_t e0, e1;

@@ -96,6 +96,10 @@ struct TiledArgs {
     // scorer uses them); zero_first = 1 asks the launcher to clear them first
     // (new scratch, or a previous sequence that did not complete)
     int zero_first;
+    // work items in the order the scorers take them (k_tile_scan): every full
+    // chunk first, then the partial (last) chunks by decreasing size, so the
+    // dynamic queues end on the shortest items; int2 = (tile, chunk index)
+    int2* items;
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).

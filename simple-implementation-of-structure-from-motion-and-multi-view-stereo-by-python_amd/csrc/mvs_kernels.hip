@@ -567,36 +567,68 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     }
 }
 
-// Exclusive scans of tile counts and work items (one workgroup).
+// Exclusive scans of tile counts and work items (one workgroup), and the
+// work-item list in longest-first order: all full chunks (tile-major), then
+// the partial chunks by decreasing candidate count.  A dynamic queue handed
+// out in that order ends on its shortest items, which trims the tail where
+// a few workgroups still run while the rest of the chip idles.
 __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
-    __shared__ int32_t part_c[1024], part_i[1024];
+    __shared__ int32_t part_c[1024], part_i[1024], part_f[1024];
+    __shared__ int32_t hist[1025];                 // partial-chunk sizes (chunk <= 1024)
     const int tid = threadIdx.x;
     const int per = (t.ntiles + 1023) / 1024;
     const int b = tid * per, e = min(b + per, t.ntiles);
-    int32_t sc = 0, si = 0;
+    int32_t sc = 0, si = 0, sf = 0;
     for (int k = b; k < e; ++k) {
         const int c = t.tile_count[k];
         sc += c;
         si += (c + t.chunk - 1) / t.chunk;
+        sf += c / t.chunk;
     }
     part_c[tid] = sc;
     part_i[tid] = si;
+    part_f[tid] = sf;
+    for (int s = tid; s <= 1024; s += 1024) hist[s] = 0;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
         int32_t vc = tid >= off ? part_c[tid - off] : 0;
         int32_t vi = tid >= off ? part_i[tid - off] : 0;
+        int32_t vf = tid >= off ? part_f[tid - off] : 0;
         __syncthreads();
         part_c[tid] += vc;
         part_i[tid] += vi;
+        part_f[tid] += vf;
         __syncthreads();
     }
-    int32_t rc = tid ? part_c[tid - 1] : 0, ri = tid ? part_i[tid - 1] : 0;
+    const int32_t n_full = part_f[1023];
+    if (t.items)
+        for (int k = b; k < e; ++k) {
+            const int rem = t.tile_count[k] % t.chunk;
+            if (rem) atomicAdd(&hist[rem], 1);
+        }
+    __syncthreads();
+    if (t.items && tid == 0) {       // descending exclusive prefix: hist[s] = partials longer than s
+        int32_t run = 0;
+        for (int s = t.chunk - 1; s >= 1; --s) {
+            const int32_t h = hist[s];
+            hist[s] = run;
+            run += h;
+        }
+    }
+    __syncthreads();
+    int32_t rc = tid ? part_c[tid - 1] : 0, ri = tid ? part_i[tid - 1] : 0, rf = tid ? part_f[tid - 1] : 0;
     for (int k = b; k < e; ++k) {
         t.tile_off[k] = rc;
         t.item_off[k] = ri;
         const int c = t.tile_count[k];
         rc += c;
         ri += (c + t.chunk - 1) / t.chunk;
+        if (t.items) {
+            const int full = c / t.chunk, rem = c - full * t.chunk;
+            for (int j = 0; j < full; ++j) t.items[rf + j] = make_int2(k, j);
+            rf += full;
+            if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int2(k, full);
+        }
         t.tile_count[k] = 0;          // clean for the next batch's k_bin
     }
     if (tid == 1023) {
@@ -930,13 +962,10 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
         const int item = __builtin_amdgcn_readfirstlane(s_item);
         if (item >= n_items) break;
         STAMP(0);
-        int lo = 0, hi = t.ntiles;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (t.item_off[mid] <= item) lo = mid; else hi = mid;
-        }
-        const int tile = lo;
-        const int chunk = item - t.item_off[tile];
+        // longest-first item list (k_tile_scan); uniform address -> scalar load
+        const unsigned long long itv =
+            *(const __attribute__((address_space(4))) unsigned long long*)(t.items + item);
+        const int tile = (int)(uint32_t)itv, chunk = (int)(uint32_t)(itv >> 32);
         const int cb = t.tile_off[tile] + chunk * t.chunk;
         const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
         const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
@@ -1147,13 +1176,9 @@ __global__ __launch_bounds__(kTGThreads, 3) void k_score_tiledg(const SceneDev s
         const int kc = k / NG, g = k - kc * NG;
         const int item = xq + 8 * kc;
         const int vb = 64 * g, nv = min(64, V - vb);
-        int lo = 0, hi = t.ntiles;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (t.item_off[mid] <= item) lo = mid; else hi = mid;
-        }
-        const int tile = lo;
-        const int chunk = item - t.item_off[tile];
+        const unsigned long long itv =
+            *(const __attribute__((address_space(4))) unsigned long long*)(t.items + item);
+        const int tile = (int)(uint32_t)itv, chunk = (int)(uint32_t)(itv >> 32);
         const int cb = t.tile_off[tile] + chunk * t.chunk;
         const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
         const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
@@ -2139,7 +2164,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant == 4 || variant == 5 || (variant == 0 && sc->mom[WID] != nullptr)) {
-        if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kChunk) return -3;
+        if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kChunk || t->items == nullptr) return -3;
         const size_t outs = (size_t)t->chunk * (8 + 8 + 4 + 4);
         const bool smem = variant == 4;
         {
@@ -2178,7 +2203,7 @@ int launch_score_tiledg_w(const SceneDev* sc, const ScoreArgs* a, const TiledArg
         t->groups != (sc->V + 63) / 64 || t->part_cnt == nullptr || t->part_sum == nullptr ||
         t->tw != kTW || t->th != kTH)
         return -3;
-    if (t->xq == nullptr) return -3;
+    if (t->xq == nullptr || t->items == nullptr) return -3;
     if (t->zero_first &&
         (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess ||
          hipMemsetAsync(t->xq, 0, sizeof(int32_t) * 8, s) != hipSuccess))
