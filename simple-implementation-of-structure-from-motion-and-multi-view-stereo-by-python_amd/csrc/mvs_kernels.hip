@@ -572,51 +572,82 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
 // the partial chunks by decreasing candidate count.  A dynamic queue handed
 // out in that order ends on its shortest items, which trims the tail where
 // a few workgroups still run while the rest of the chip idles.
+// Inclusive scan of N values per thread over a 1024-thread block: wave scans
+// by __shfl_up, the 16 wave totals scanned by one wave, two barriers.
+template <int N>
+DEV void block_scan_1024(int32_t (&v)[N], int32_t* wtot /* LDS, 16 * N */) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t y = __shfl_up(v[k], off, 64);
+            if (lane >= off) v[k] += y;
+        }
+    if (lane == 63)
+#pragma unroll
+        for (int k = 0; k < N; ++k) wtot[wave * N + k] = v[k];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            int32_t x = lane < 16 ? wtot[lane * N + k] : 0;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                const int32_t y = __shfl_up(x, off, 64);
+                if (lane >= off) x += y;
+            }
+            if (lane < 16) wtot[lane * N + k] = x;
+        }
+    }
+    __syncthreads();
+    if (wave > 0)
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] += wtot[(wave - 1) * N + k];
+}
+
+// Exclusive scans of tile counts and work items (one workgroup), and the
+// work-item list in longest-first order: all full chunks (tile-major), then
+// the partial chunks by decreasing candidate count.  A dynamic queue handed
+// out in that order ends on its shortest items, which trims the tail where
+// a few workgroups still run while the rest of the chip idles.
 __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
-    __shared__ int32_t part_c[1024], part_i[1024], part_f[1024];
+    __shared__ int32_t wtot[16 * 3];
+    __shared__ int32_t tot[3];
     __shared__ int32_t hist[1025];                 // partial-chunk sizes (chunk <= 1024)
     const int tid = threadIdx.x;
     const int per = (t.ntiles + 1023) / 1024;
     const int b = tid * per, e = min(b + per, t.ntiles);
-    int32_t sc = 0, si = 0, sf = 0;
+    int32_t v3[3] = {0, 0, 0};                     // candidates, items, full chunks of my tiles
     for (int k = b; k < e; ++k) {
         const int c = t.tile_count[k];
-        sc += c;
-        si += (c + t.chunk - 1) / t.chunk;
-        sf += c / t.chunk;
+        v3[0] += c;
+        v3[1] += (c + t.chunk - 1) / t.chunk;
+        v3[2] += c / t.chunk;
     }
-    part_c[tid] = sc;
-    part_i[tid] = si;
-    part_f[tid] = sf;
+    const int32_t own[3] = {v3[0], v3[1], v3[2]};
     for (int s = tid; s <= 1024; s += 1024) hist[s] = 0;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        int32_t vc = tid >= off ? part_c[tid - off] : 0;
-        int32_t vi = tid >= off ? part_i[tid - off] : 0;
-        int32_t vf = tid >= off ? part_f[tid - off] : 0;
-        __syncthreads();
-        part_c[tid] += vc;
-        part_i[tid] += vi;
-        part_f[tid] += vf;
-        __syncthreads();
-    }
-    const int32_t n_full = part_f[1023];
+    block_scan_1024<3>(v3, wtot);
+    if (tid == 1023) { tot[0] = v3[0]; tot[1] = v3[1]; tot[2] = v3[2]; }
     if (t.items)
         for (int k = b; k < e; ++k) {
             const int rem = t.tile_count[k] % t.chunk;
             if (rem) atomicAdd(&hist[rem], 1);
         }
     __syncthreads();
-    if (t.items && tid == 0) {       // descending exclusive prefix: hist[s] = partials longer than s
-        int32_t run = 0;
-        for (int s = t.chunk - 1; s >= 1; --s) {
-            const int32_t h = hist[s];
-            hist[s] = run;
-            run += h;
-        }
+    const int32_t n_full = tot[2];
+    {
+        // descending exclusive prefix, hist[s] = partials longer than s, as a
+        // scan over the sizes in reverse order (thread i <-> size chunk-1-i)
+        const int nsz = t.chunk - 1;
+        const int32_t mine = (t.items && tid < nsz) ? hist[t.chunk - 1 - tid] : 0;
+        int32_t r1[1] = {mine};
+        __syncthreads();                            // everyone has read hist before it is rewritten
+        block_scan_1024<1>(r1, wtot);
+        if (t.items && tid < nsz) hist[t.chunk - 1 - tid] = r1[0] - mine;
+        __syncthreads();
     }
-    __syncthreads();
-    int32_t rc = tid ? part_c[tid - 1] : 0, ri = tid ? part_i[tid - 1] : 0, rf = tid ? part_f[tid - 1] : 0;
+    int32_t rc = v3[0] - own[0], ri = v3[1] - own[1], rf = v3[2] - own[2];
     for (int k = b; k < e; ++k) {
         t.tile_off[k] = rc;
         t.item_off[k] = ri;
@@ -632,8 +663,8 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
         t.tile_count[k] = 0;          // clean for the next batch's k_bin
     }
     if (tid == 1023) {
-        t.tile_off[t.ntiles] = part_c[1023];
-        t.item_off[t.ntiles] = part_i[1023];
+        t.tile_off[t.ntiles] = tot[0];
+        t.item_off[t.ntiles] = tot[1];
     }
     // work-queue heads and the fix-list length start this batch at zero
     if (tid == 0) {
