@@ -1963,6 +1963,8 @@ __global__ __launch_bounds__(kM2Threads, 3) void k_score_mfma2(const SceneDev sc
 // Re-scores the candidates k_score_tiled3 flagged (a view decision inside the
 // guard band) with the direct scorer, whose guard lanes take the numpy-order
 // ctNcc; overwrites their mask/count/avg.  One wave per flagged candidate.
+constexpr int kFixBlocks = 256;   // one wave per flagged candidate in one round for <= 1024 of them
+
 template <int WID, int NS = 1>
 __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t) {
@@ -2175,7 +2177,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
                 default: launch_mfma2<WID, 4>(sc, a, t, s); break;
             }
         }
-        hipLaunchKernelGGL(k_score_fix<WID>, dim3(64), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant == 6) {
@@ -2191,7 +2193,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
                 default: launch_mfma<WID, 4>(sc, a, t, s); break;
             }
         }
-        hipLaunchKernelGGL(k_score_fix<WID>, dim3(64), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant == 4 || variant == 5 || (variant == 0 && sc->mom[WID] != nullptr)) {
@@ -2210,7 +2212,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
             else hipLaunchKernelGGL((k_score_tiled3<WID, 64, 0>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
         }
         }
-        hipLaunchKernelGGL(k_score_fix<WID>, dim3(64), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     TimedLaunch tl(s, ev0, ev1);
@@ -2254,9 +2256,9 @@ int launch_score_tiledg_w(const SceneDev* sc, const ScoreArgs* a, const TiledArg
     }
     hipLaunchKernelGGL(k_group_finalize, dim3(nb), dim3(256), 0, s, *a, *t, (2 * WID + 1) * (2 * WID + 1));
     if (sc->V <= 128)
-        hipLaunchKernelGGL((k_score_fix<WID, 2>), dim3(64), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL((k_score_fix<WID, 2>), dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
     else
-        hipLaunchKernelGGL((k_score_fix<WID, 4>), dim3(64), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL((k_score_fix<WID, 4>), dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
