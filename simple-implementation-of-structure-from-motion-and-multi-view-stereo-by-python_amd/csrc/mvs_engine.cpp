@@ -1387,6 +1387,8 @@ int mvs_harris_points(mvs_ctx* ctx, int view, int32_t* out, int64_t cap, int64_t
     return guarded(ctx, [&]() -> int {
         if (!n_out || (cap > 0 && !out)) throw Fail{MVS_E_ARG, "null output"};
         if (view < 0 || view >= ctx->V) throw Fail{MVS_E_ARG, "view out of range"};
+        // BORDER_REFLECT_101 of a 3x3 Sobel needs two pixels per axis
+        if (ctx->H < 2 || ctx->W < 2) throw Fail{MVS_E_UNSUPPORTED, "Harris needs images of at least 2x2"};
         const int64_t npx = (int64_t)ctx->H * ctx->W;
         ctx->f_resp.ensure(npx);
         ctx->f_dil.ensure(npx);
