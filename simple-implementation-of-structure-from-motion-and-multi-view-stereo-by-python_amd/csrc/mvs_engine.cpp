@@ -341,8 +341,13 @@ struct mvs_ctx {
 };
 
 struct mvs_stage;
+// The stage's outputs as record indices into the records' centres and
+// colours; mvs_stage_rows writes the [x y z r g b] rows straight into the
+// caller's buffer (no intermediate copy of the ~35 MB of rows).
 struct mvs_stage_result {
-    std::vector<double> initial, all;
+    std::vector<double> c;          // nrec * 3
+    std::vector<uint8_t> color;     // nrec * 4
+    std::vector<int32_t> initial, all;   // record per output row
     int64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
@@ -883,20 +888,17 @@ struct Engine {
 
     void output(mvs_stage_result* res) {
         double ta = now();
-        std::vector<double> hc(nrec * 3);
-        std::vector<uint8_t> hcol(nrec * 4);
+        res->c.resize(nrec * 3);
+        res->color.resize(nrec * 4);
         if (nrec) {
-            HIPCHK(hipMemcpyAsync(hc.data(), d_c.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(hcol.data(), d_color.p, nrec * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(res->c.data(), d_c.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(res->color.data(), d_color.p, nrec * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
         double tb = now();
         t_out[0] = tb - ta;
-        auto row = [&](std::vector<double>& out, int64_t r) {
-            out.push_back(hc[3 * r]); out.push_back(hc[3 * r + 1]); out.push_back(hc[3 * r + 2]);
-            out.push_back(hcol[4 * r]); out.push_back(hcol[4 * r + 1]); out.push_back(hcol[4 * r + 2]);
-        };
-        for (int64_t r = 0; r < n_seeds; ++r) row(res->initial, r);
+        res->initial.resize(n_seeds);
+        for (int64_t r = 0; r < n_seeds; ++r) res->initial[r] = (int32_t)r;
         // stable sort of the events by key (min view, cell x, cell y): LSD radix
         // sort, 11 bits per pass (the key space is V * nci * ncj)
         std::vector<uint64_t> keyed, tmp;   // key << 32 | event index
@@ -923,8 +925,8 @@ struct Engine {
         }
         double td = now();
         t_out[2] = td - tc;
-        res->all.reserve(keyed.size() * 6);
-        for (uint64_t k : keyed) row(res->all, events[(uint32_t)k]);
+        res->all.resize(keyed.size());
+        for (size_t i = 0; i < keyed.size(); ++i) res->all[i] = events[(uint32_t)keyed[i]];
         t_out[3] = now() - td;
         res->stats[0] = stat_pops;
         res->stats[1] = stat_tests;
@@ -1290,13 +1292,24 @@ void mvs_stage_destroy(mvs_stage* st) {
 
 int64_t mvs_stage_count(const mvs_stage_result* res, int which) {
     if (!res) return MVS_E_ARG;
-    return (int64_t)((which ? res->all.size() : res->initial.size()) / 6);
+    return (int64_t)(which ? res->all.size() : res->initial.size());
 }
 
 int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows) {
     if (!res || !rows) return MVS_E_ARG;
-    const std::vector<double>& v = which ? res->all : res->initial;
-    std::memcpy(rows, v.data(), v.size() * sizeof(double));
+    const std::vector<int32_t>& idx = which ? res->all : res->initial;
+    const double* c = res->c.data();
+    const uint8_t* col = res->color.data();
+    for (size_t i = 0; i < idx.size(); ++i) {
+        const int64_t r = idx[i];
+        double* o = rows + 6 * i;
+        o[0] = c[3 * r];
+        o[1] = c[3 * r + 1];
+        o[2] = c[3 * r + 2];
+        o[3] = col[4 * r];
+        o[4] = col[4 * r + 1];
+        o[5] = col[4 * r + 2];
+    }
     return 0;
 }
 
