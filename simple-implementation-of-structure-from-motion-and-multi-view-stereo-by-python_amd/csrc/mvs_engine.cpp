@@ -500,7 +500,7 @@ struct Engine {
     std::vector<uint8_t> h_accept, h_enq;
     std::vector<int64_t> h_child;   // first child record, -1 = unscored
 
-    std::vector<uint8_t> table;     // V*nci*ncj, 1 = vacant (CellTable)
+    std::vector<uint64_t> table;    // [nci][ncj][words] view bitmasks, 1 = vacant (CellTable)
     std::vector<int32_t> events;    // accepted patch objects, in fill order
     int64_t n_seeds = 0;
     int64_t stat_tests = 0, stat_scored = 0, stat_sweeps = 0, stat_seed_cands = 0;
@@ -536,22 +536,18 @@ struct Engine {
     bool vacant(int v, long ci, long cj) const {
         if (ci >= nci || ci < 0) return false;
         if (cj >= ncj || cj < 0) return false;
-        return table[((int64_t)v * nci + ci) * ncj + cj] != 0;
+        return (table[((int64_t)ci * ncj + cj) * words + (v >> 6)] >> (v & 63)) & 1u;
     }
 
     // CellTable.fill_with_point for every V entry of record r (MVS2.py:98-107,
     // 258-259, 401-402); the Q-table side is reconstructed from `events`.
     void fill_record(int64_t r) {
+        // every V entry carries the same projection, so one cell gets the
+        // record's whole view mask: clear those views' vacancy bits at once
         const int cx = h_cell[2 * r], cy = h_cell[2 * r + 1];
-        for (int w = 0; w < words; ++w) {
-            uint64_t m = h_mask[r * words + w];
-            while (m) {
-                const int v = 64 * w + __builtin_ctzll(m);
-                m &= m - 1;
-                if (cx >= 0 && cx < nci && cy >= 0 && cy < ncj)
-                    table[((int64_t)v * nci + cx) * ncj + cy] = 0;
-            }
-        }
+        if (cx < 0 || cx >= nci || cy < 0 || cy >= ncj) return;
+        uint64_t* cell = &table[((int64_t)cx * ncj + cy) * words];
+        for (int w = 0; w < words; ++w) cell[w] &= ~h_mask[r * words + w];
     }
 
     void fetch_range(int64_t first, int64_t n) {
@@ -962,7 +958,14 @@ Engine* make_engine(mvs_ctx* ctx, int cell_size, double scale, int wid, int64_t 
     E->ncj = (int)std::ceil((double)(ctx->H - 1) / cell_size);
     E->max_pops = std::min<int64_t>(std::max<int64_t>(max_pops, 0), 100000);   // MVS2.py:321
     E->s = ctx->stream;
-    E->table.assign((size_t)ctx->V * E->nci * E->ncj, 1);
+    // CellTable as vacancy bitmasks, one per cell: bit v of cell (ci, cj) = 1
+    // while view v's cell is vacant (np.ones, MVS2.py:88)
+    E->table.assign((size_t)E->nci * E->ncj * E->words, 0);
+    for (int64_t k = 0; k < (int64_t)E->nci * E->ncj; ++k)
+        for (int w = 0; w < E->words; ++w) {
+            const int nv = std::min(64, ctx->V - 64 * w);
+            E->table[k * E->words + w] = nv >= 64 ? ~0ull : ((1ull << nv) - 1ull);
+        }
     return E.release();
 }
 
