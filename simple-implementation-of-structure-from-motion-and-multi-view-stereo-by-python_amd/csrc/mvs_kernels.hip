@@ -1105,8 +1105,10 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
                     pass = z > tk;
                     ncc = z;
                 } else {
+                    // the reference view's n S_aa - S_a^2 from its (wave-uniform) w: lane R
+                    // itself is not live, so its lane value cannot be read back here
                     const int32_t db = mom_db(mb);
-                    const int32_t da = __builtin_amdgcn_readlane(db, R);
+                    const int32_t da = mom_db(MomEntry{wa, 0u});
                     ncc = ((double)num * (double)NPX) /
                           ((double)(NPX - 1) * sqrt((double)da * (double)db));
                     guard = fabs(ncc - a.thr) <= kGuard;

@@ -56,7 +56,8 @@ def test_photo_test_vs_reference_golden(ctx, func_golden):
         np.testing.assert_allclose(avg, f["pt_avg"][sel], rtol=0, atol=AVG_TOL)
 
 
-@pytest.mark.parametrize("wid,thr", [(5, 0.7), (5, 0.4), (3, 0.7), (1, 0.5), (2, 0.6), (4, 0.7)])
+@pytest.mark.parametrize("wid,thr", [(5, 0.7), (5, 0.4), (3, 0.7), (1, 0.5), (2, 0.6), (4, 0.7),
+                                     (5, 0.005), (5, -0.3), (3, -0.9)])
 def test_score_vs_oracle_bench_batch(kctx, oracle_scene, dino, wid, thr):
     rgb, K, R, t = dino
     c, ref = bench_candidates(6000, K, R, t, seed=wid)
@@ -271,7 +272,7 @@ def _smooth_ring(pkg, V, H=96, W=128):
     return rgb, K, R, t
 
 
-@pytest.mark.parametrize("V,wid", [(68, 5), (100, 3), (256, 3)])
+@pytest.mark.parametrize("V,wid", [(68, 5), (100, 3), (256, 3), (100, 1), (132, 2), (200, 4)])
 def test_view_groups_wid_and_partial_group(pkg, orc, V, wid):
     """k_score_tiledg with a 4-view last group (V = 68) and at wid 3."""
     H, W = 96, 128
@@ -316,7 +317,7 @@ def test_view_groups_threshold_on_reference_value(pkg, orc):
         assert cx.exact_hits() > hits0
 
 
-@pytest.mark.parametrize("V", [5, 100, 102, 192, 256])
+@pytest.mark.parametrize("V", [5, 32, 64, 100, 102, 192, 256])
 def test_view_count_variants(pkg, orc, V):
     """Lane-slot layouts: V < 64, one extra slot, and the 4-slot 256-view case;
     3000 candidates take the tiled scorers (k_score_tiled3, or the view-group
