@@ -402,7 +402,9 @@ DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fe
             }
         }
         const uint64_t m = __ballot(pass);
-        if (lane == 0) mask_out[s] = m;
+        // NS slots can exceed the candidate's ceil(V/64) mask words (NS = 4 for
+        // 128 < V <= 192): only the words that exist are written
+        if (lane == 0 && 64 * s < V) mask_out[s] = m;
         cnt += __popcll(m);
         acc += pass ? ncc : 0.0;
     }
@@ -436,9 +438,9 @@ DEV void wave_score(const SceneDev& sc, int R, int q, int r, double thr, uint64_
 }
 
 template <int NS>
-DEV void wave_score_empty(uint64_t* mask_out, int32_t* count_out, double* avg_out) {
+DEV void wave_score_empty(uint64_t* mask_out, int32_t* count_out, double* avg_out, int words) {
     const int lane = threadIdx.x & 63;
-    if (lane < NS) mask_out[lane] = 0;
+    if (lane < NS && lane < words) mask_out[lane] = 0;
     if (lane == 0) {
         *count_out = 0;
         if (avg_out) *avg_out = 0.0;
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
     if (lane == 0) { a.xy[2 * cand] = px; a.xy[2 * cand + 1] = py; }
     int q, r;
     if (!window_ok(sc, px, py, WID, &q, &r)) {
-        wave_score_empty<NS>(a.mask + cand * words, a.count + cand, a.avg ? a.avg + cand : nullptr);
+        wave_score_empty<NS>(a.mask + cand * words, a.count + cand, a.avg ? a.avg + cand : nullptr, words);
         return;
     }
     q = __builtin_amdgcn_readfirstlane(q);
@@ -2058,7 +2060,7 @@ __global__ __launch_bounds__(256) void k_expand(const SceneDev sc, RecordsDev re
     }
     int q, r;
     if (!window_ok(sc, px, py, WID, &q, &r)) {
-        wave_score_empty<NS>(rec.mask + out * words, rec.count + out, nullptr);
+        wave_score_empty<NS>(rec.mask + out * words, rec.count + out, nullptr, words);
         if (lane == 0) rec.accept[out] = 0;
         return;
     }

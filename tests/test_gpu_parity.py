@@ -524,3 +524,24 @@ def test_ring256_quarter_sweep(pkg, orc):
     for g, e in zip(got[:3], exp[:3]):
         assert np.array_equal(g, e)
     np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+
+
+@pytest.mark.parametrize("V,n", [(132, 2500), (160, 500), (160, 2500), (44, 600)])
+def test_mask_words_and_zero_threshold(pkg, orc, V, n):
+    """128 < V <= 192 runs 4 view slots for 3 mask words: no slot may write past
+    its candidate (direct path at n < 2048, guard re-score of the view-group
+    scorer at thr 0, where num == 0 lanes take the numpy-order path); widths
+    that are not a multiple of 4."""
+    H, W = 67, 81
+    rgb, K, R, t = pkg.synthetic.ring_scene(V=V, H=H, W=W, seed=V + 1000)
+    rgb = ((rgb.astype(np.uint16) + np.roll(rgb, 1, axis=0) + np.roll(rgb, 1, axis=1)) // 3).astype(np.uint8)
+    sc = orc.Scene(rgb, K, R, t)
+    c, ref = pkg.synthetic.candidates(n, K, R, t, W=W, H=H, seed=V)
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        for wid in (1, 5):
+            for thr in (0.0, -0.5, 0.7):
+                got = cx.score(c, ref, thr, wid)
+                exp = sc.score_batch(c, ref, thr, wid)
+                for g, e in zip(got[:3], exp[:3]):
+                    assert np.array_equal(g, e), (wid, thr)
+                np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
