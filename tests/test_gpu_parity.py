@@ -545,3 +545,47 @@ def test_mask_words_and_zero_threshold(pkg, orc, V, n):
                 for g, e in zip(got[:3], exp[:3]):
                     assert np.array_equal(g, e), (wid, thr)
                 np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+
+
+@pytest.mark.parametrize("V,pops,world", [(24, 2000, 1), (70, 800, 2), (150, 250, 3)])
+def test_stage_sphere_scene(pkg, orc, V, pops, world):
+    """The whole stage on a geometrically consistent synthetic scene (textured
+    sphere, ring cameras) with 1, 2 and 3 mask words per record (V 24 / 70 /
+    150): GPU single-rank run and the emulated multi-rank protocol against the
+    oracle, bit-exact."""
+    import torch
+    rgb, K, R, t, off, ov, oxy = pkg.synthetic.sphere_scene(V=V, seed=V)
+    oini, oall, ost = orc.Scene(rgb, K, R, t).mvs_stage(off, ov, oxy, scale=10.0, max_pops=pops)
+    assert len(oall) > 1000
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        ini, allp, st = cx.stage(off, ov, oxy, cell_size=2, scale=10.0, wid=5, max_pops=pops)
+    assert np.array_equal(ini, oini) and np.array_equal(allp, oall)
+    assert st["tests"] == ost["tests"] and st["queue_left"] == ost["queue_left"]
+    if world == 1:
+        return
+    ctxs = [pkg.MvsContext(rgb, K, R, t, device=0) for _ in range(world)]
+    try:
+        sts = [c.stage_begin(off, ov, oxy, cell_size=2, scale=10.0, wid=5, max_pops=pops, rank=r,
+                             world=world) for r, c in enumerate(ctxs)]
+        dev = torch.device("cuda", 0)
+        while True:
+            njs = [s.plan() for s in sts]
+            assert len(set(njs)) == 1
+            if njs[0] == 0:
+                break
+            smax = sts[0].slice_max(njs[0])
+            outs = [torch.full((smax, sts[0].width), -7, dtype=torch.int64, device=dev)
+                    for _ in range(world)]
+            for s, o in zip(sts, outs):
+                s.score_slice(o)
+            allbuf = torch.stack(outs)
+            for s in sts:
+                s.ingest(allbuf)
+        res = [s.finish() for s in sts]
+        for s in sts:
+            s.close()
+    finally:
+        for c in ctxs:
+            c.close()
+    for ini_r, allp_r, _ in res:
+        assert np.array_equal(ini_r, oini) and np.array_equal(allp_r, oall)
