@@ -128,7 +128,9 @@ void mvs_stage_free(mvs_stage_result* res);
  *                                    (world > 1; may be NULL when world == 1)
  *   <all-gather the slices, e.g. RCCL>
  *   mvs_stage_ingest(st, all)        all[world][ceil(nj/world)][width] (device):
- *                                    every rank's records into the record table
+ *                                    every rank's records into the record table;
+ *                                    `all` must be complete when called (the
+ *                                    context's stream waits for no other stream)
  * and ends with mvs_stage_finish (same result as mvs_stage_run) and
  * mvs_stage_destroy.  width = mvs_stage_record_width(st) int64 words.  Seeding
  * is replicated on every rank; the commit is identical on every rank because

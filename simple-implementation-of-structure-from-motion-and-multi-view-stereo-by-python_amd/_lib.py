@@ -375,7 +375,13 @@ class Stage:
         check(load().mvs_stage_score_slice(self._st, ptr), self.ctx.handle, "mvs_stage_score_slice")
 
     def ingest(self, gathered=None):
-        """gathered = device int64 tensor (world, slice_max, width) when world > 1."""
+        """gathered = device int64 tensor (world, slice_max, width) when world > 1.
+
+        The library reads it on its own stream, which does not wait for torch's:
+        the producer (all-gather, torch.stack) is synchronised here first."""
+        if gathered is not None and getattr(gathered, "is_cuda", False):
+            import torch
+            torch.cuda.current_stream(gathered.device).synchronize()
         ptr = gathered.data_ptr() if gathered is not None else None
         check(load().mvs_stage_ingest(self._st, ptr), self.ctx.handle, "mvs_stage_ingest")
 

@@ -109,12 +109,72 @@ DEV double exact_ncc_generic(FA&& A, FB&& B, int n) {
     return s / (n - 1);
 }
 
+// ctNcc in numpy's order with the pixel count known at compile time: every
+// loop unrolls, so pixel i's byte comes from a register (constant index).
+template <int N, class FA, class FB>
+DEV double exact_ncc_fixed(FA&& A, FB&& B) {
+    int sa = 0, sb = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) { sa += A(i); sb += B(i); }
+    const double ma = (double)sa / N, mb = (double)sb / N;
+    auto pairwise = [&](auto&& X, double m) {
+        // numpy pairwise sum of (x - m)^2 for N <= 128: 8 accumulators
+        if constexpr (N < 8) {
+            double res = 0.;
+#pragma unroll
+            for (int i = 0; i < N; i++) { const double x = X(i) - m; res += x * x; }
+            return res;
+        } else {
+            double acc[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) { const double x = X(j) - m; acc[j] = x * x; }
+#pragma unroll
+            for (int i = 8; i < N - (N % 8); i += 8)
+#pragma unroll
+                for (int j = 0; j < 8; j++) { const double x = X(i + j) - m; acc[j] += x * x; }
+            double res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+            for (int i = N - (N % 8); i < N; i++) { const double x = X(i) - m; res += x * x; }
+            return res;
+        }
+    };
+    static_assert(N <= 128, "numpy pairwise summation restated for n <= 128");
+    const double stda = sqrt(pairwise([&](int i) { return (double)A(i); }, ma) / N);
+    const double stdb = sqrt(pairwise([&](int i) { return (double)B(i); }, mb) / N);
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) s = s + (((double)A(i) - ma) / stda) * (((double)B(i) - mb) / stdb);
+    return s / (N - 1);
+}
+
+// The two windows are loaded once as aligned dwords (NB rows of NW+1 quads,
+// the same reads wave_score issues) and re-aligned in registers; the numpy-
+// order arithmetic then runs on registers instead of re-reading ~6 bytes of
+// the stack per pixel (the guard path used to wait on ~700 dependent loads).
 template <int WID>
-__device__ __forceinline__ double exact_ncc_stack(const SceneDev sc, int R, int v, int q, int r) {
-    constexpr int NB = 2 * WID + 1;
-    auto A = [&](int i) -> int { return stack_px(sc, R, r - WID + i / NB, q - WID + i % NB); };
-    auto B = [&](int i) -> int { return stack_px(sc, v, r - WID + i / NB, q - WID + i % NB); };
-    return exact_ncc_generic(A, B, NB * NB);
+__device__ __noinline__ double exact_ncc_stack(const SceneDev sc, int R, int v, int q, int r) {
+    constexpr int NB = 2 * WID + 1, NW = (NB + 3) / 4;
+    const int q0 = q - WID, o = q0 & 3;
+    const int64_t vstride = (int64_t)sc.V * 4;
+    const uint8_t* p0 = sc.stack + (int64_t)(r - WID) * sc.row_bytes + (int64_t)(q0 >> 2) * vstride;
+    uint32_t wa[NB][NW], wb[NB][NW];
+#pragma unroll
+    for (int row = 0; row < NB; ++row) {
+        uint32_t da[NW + 1], db[NW + 1];
+#pragma unroll
+        for (int j = 0; j <= NW; ++j) {
+            da[j] = *(const uint32_t*)(p0 + (int64_t)row * sc.row_bytes + j * vstride + R * 4);
+            db[j] = *(const uint32_t*)(p0 + (int64_t)row * sc.row_bytes + j * vstride + v * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            wa[row][j] = __builtin_amdgcn_alignbyte(da[j + 1], da[j], o);
+            wb[row][j] = __builtin_amdgcn_alignbyte(db[j + 1], db[j], o);
+        }
+    }
+    auto A = [&](int i) -> int { return (int)((wa[i / NB][(i % NB) >> 2] >> (8 * ((i % NB) & 3))) & 0xffu); };
+    auto B = [&](int i) -> int { return (int)((wb[i / NB][(i % NB) >> 2] >> (8 * ((i % NB) & 3))) & 0xffu); };
+    return exact_ncc_fixed<NB * NB>(A, B);
 }
 
 // Wave-wide binary64 sum without LDS: DPP butterflies inside each row of 16
