@@ -1209,6 +1209,250 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
 
 
 // ---------------------------------------------------------------------------
+// Tiled scorer v4 (V <= 64, variant 11, not the default): k_score_tiled3's work split and
+// arithmetic, with every window read an 8-byte-aligned ds_read_b64.  On gfx950
+// a ds_read_b64 moves 8 B per lane in ~2.7 LDS cycles per wave-instruction,
+// a ds_read2_b32 in ~4.4 (tools/ubench/lds_b64.hip), and the LDS pipe bounds
+// this kernel.  The region image is kept twice, as pairs of adjacent quads
+// [row][pair][view][2 dwords]: pairs (0,1), (2,3), ... in the even image and
+// (1,2), (3,4), ... in the odd one, so a window row starting at quad k0 is
+// ceil(NQ/2) aligned b64 reads from image (k0 & 1), lane v at dword 2v (64
+// banks, no conflict); the reference view's quads are the same reads at lane
+// R's address (broadcast).  The doubled image (55 KB at wid 5, V = 48) is
+// shared by 8 waves, so two workgroups per CU keep 4 waves per SIMD.
+constexpr int kT4Threads = 512, kT4Waves = kT4Threads / 64, kStage4 = 4;
+
+template <int WID>
+struct PairGeom {
+    using G = TileGeom<WID>;
+    // pairs per region row (both images): the largest (k0 >> 1) + ceil(NQ_o / 2)
+    // over window byte offsets o and first quads k0 whose window fits the region
+    static constexpr int np() {
+        int m = 0;
+        for (int o = 0; o < 4; ++o) {
+            const int nq = (o + G::NB + 3) / 4;
+            for (int k0 = 0; k0 + nq <= G::NQ; ++k0) {
+                const int v = (k0 >> 1) + (nq + 1) / 2;
+                if (v > m) m = v;
+            }
+        }
+        return m;
+    }
+    // ... and room for every staged quad (even image: pair NQ-1 >> 1)
+    static constexpr int NP = np() > (G::NQ + 1) / 2 ? np() : (G::NQ + 1) / 2;
+};
+
+template <int WID, int O, int RS, int PS>
+DEV uint32_t sab_pairs(const uint32_t* own_g, const uint32_t* ref_g, uint32_t zm) {
+    using M = QuadMasks<WID, O>;
+    constexpr int NB = 2 * WID + 1;
+    constexpr int NPR = (M::NQ + 1) / 2;   // b64 reads per row
+    using lds_u64 = __attribute__((address_space(3))) const unsigned long long;
+    unsigned long long d[NB][NPR], e[NB][NPR];
+#pragma unroll
+    for (int p = 0; p < NPR; ++p) {
+        lds_u64* o = (lds_u64*)(own_g + p * PS);
+        lds_u64* r = (lds_u64*)(ref_g + p * PS);
+        asm volatile("" : "+v"(o));
+        asm volatile("" : "+v"(r));
+#pragma unroll
+        for (int row = 0; row < NB; ++row) {
+            d[row][p] = o[row * (RS / 2)];
+            e[row][p] = r[row * (RS / 2)];
+        }
+    }
+    uint32_t ab[M::NQ];
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) ab[jj] = 0;
+#pragma unroll
+    for (int row = 0; row < NB; ++row)
+#pragma unroll
+        for (int jj = 0; jj < M::NQ; ++jj) {
+            const uint32_t m = M::mask(jj);
+            const uint32_t ev = (uint32_t)(e[row][jj >> 1] >> (32 * (jj & 1)));
+            const uint32_t dv = (uint32_t)(d[row][jj >> 1] >> (32 * (jj & 1)));
+            const uint32_t am = (m == 0xffffffffu) ? ev : (ev & m);
+            ab[jj] = __builtin_amdgcn_udot4(am, dv, ab[jj], false);
+        }
+    if constexpr (M::NQ & 1) {
+        // the last pair's upper quad lies past the window: "use" it (times the
+        // opaque zero zm) so the own read stays a ds_read_b64 -- as a
+        // ds_read_b32 at lane stride 2 dwords it would take a 2-way bank
+        // conflict (~4.2 LDS cycles against ~2.8).  The broadcast side may
+        // narrow: same-address reads do not conflict.
+#pragma unroll
+        for (int row = 0; row < NB; ++row)
+            ab[0] = __builtin_amdgcn_udot4(zm, (uint32_t)(d[row][NPR - 1] >> 32), ab[0], false);
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) sum += ab[jj];
+    return sum;
+}
+
+template <int WID, int QS>
+// no-load-store-opt: the SI load/store optimizer would pair the row reads
+// into ds_read2_b64 (8 LDS cycles per 16 B, as slow as ds_read2_b32)
+__global__ __launch_bounds__(kT4Threads, 4) __attribute__((target("no-load-store-opt"))) void k_score_tiled4(const SceneDev sc, const ScoreArgs a,
+                                                                const TiledArgs t) {
+    using G = TileGeom<WID>;
+    constexpr int NB = 2 * WID + 1;
+    constexpr int NPX = NB * NB;
+    constexpr int NP = PairGeom<WID>::NP;
+    constexpr int PS = 2 * QS;               // dwords per (row, pair)
+    constexpr int RS = NP * PS;              // dwords per region row
+    constexpr int IMG = G::ROWS * RS;        // dwords per image
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int V = sc.V;
+    const int n_items = t.item_off[t.ntiles];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const MomEntry* __restrict__ mom = sc.mom[WID];
+    uint32_t zm = 0;                 // zero the compiler cannot see through (sab_pairs)
+    asm volatile("" : "+s"(zm));
+    uint64_t* o_mask = (uint64_t*)(lds + 2 * IMG);
+    double* o_avg = (double*)(o_mask + t.chunk);
+    int32_t* o_cnt = (int32_t*)(o_avg + t.chunk);
+    int32_t* o_idx = o_cnt + t.chunk;
+    __shared__ int s_item;
+    for (;;) {
+        if (threadIdx.x == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
+        __syncthreads();
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item >= n_items) break;
+        const unsigned long long itv =
+            *(const __attribute__((address_space(4))) unsigned long long*)(t.items + item);
+        const int tile = (int)(uint32_t)itv, chunk = (int)(uint32_t)(itv >> 32);
+        const int cb = t.tile_off[tile] + chunk * t.chunk;
+        const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int y0 = ty * kTH - WID;
+        const int kq0 = tx * (kTW / 4) + G::KQ0;
+        {
+            // one thread per (row, pair, view): quads 2p, 2p+1, 2p+2 of that view
+            // (dword loads, consecutive lanes = consecutive views) -> one
+            // ds_write_b64 into each image (8 contiguous bytes per lane: no
+            // bank conflict)
+            const int total = G::ROWS * NP * V;
+            for (int base = 0; base < total; base += kStage4 * kT4Threads) {
+                uint32_t g[kStage4][3];
+                int dst[kStage4];
+#pragma unroll
+                for (int u = 0; u < kStage4; ++u) {
+                    const int k = base + u * kT4Threads + (int)threadIdx.x;
+                    dst[u] = -1;
+                    g[u][0] = g[u][1] = g[u][2] = 0;
+                    if (k < total) {
+                        const int rp = k / V, v = k - rp * V;
+                        const int ry = rp / NP, pp = rp - ry * NP;
+                        const int y = y0 + ry, gq = kq0 + 2 * pp;
+                        if (y >= 0 && y < sc.H) {
+                            const uint8_t* rowb = sc.stack + (int64_t)y * sc.row_bytes + v * 4;
+#pragma unroll
+                            for (int h = 0; h < 3; ++h)
+                                if (gq + h >= 0 && gq + h < sc.Wq)
+                                    g[u][h] = *(const uint32_t*)(rowb + (int64_t)(gq + h) * V * 4);
+                        }
+                        dst[u] = ry * RS + pp * PS + 2 * v;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kStage4; ++u)
+                    if (dst[u] >= 0) {
+                        *(uint2*)(lds + dst[u]) = make_uint2(g[u][0], g[u][1]);
+                        *(uint2*)(lds + IMG + dst[u]) = make_uint2(g[u][1], g[u][2]);
+                    }
+            }
+        }
+        __syncthreads();
+        auto sload = [](const int2* p) -> int2 {
+            const unsigned long long v = *(const __attribute__((address_space(4))) unsigned long long*)p;
+            return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+        };
+        int2 cur = cb + wave < ce ? sload(t.sorted + cb + wave) : make_int2(0, 0);
+        MomEntry mb_cur{0.0, 0u};
+        if (cb + wave < ce) {
+            const int pk = cur.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
+            if (lane < V) mb_cur = load_mom(mom, (r * sc.W + q) * V + lane);
+        }
+        for (int j = cb + wave; j < ce; j += kT4Waves) {
+            const int2 nxt = j + kT4Waves < ce ? sload(t.sorted + j + kT4Waves) : make_int2(0, 0);
+            MomEntry mb_nxt{0.0, 0u};
+            if (j + kT4Waves < ce) {
+                const int pk = nxt.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
+                if (lane < V) mb_nxt = load_mom(mom, (r * sc.W + q) * V + lane);
+            }
+            const int pk = cur.y;
+            const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
+            const int q0 = q - WID, o = q0 & 3;
+            const int k0 = (q0 >> 2) - kq0;
+            const MomEntry mb = mb_cur;
+            const uint32_t ma_sb = __builtin_amdgcn_readlane(mb.sb, R);
+            const uint2 wa2 = make_uint2(__builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mb.w), R),
+                                         __builtin_amdgcn_readlane((uint32_t)((uint64_t)__double_as_longlong(mb.w) >> 32), R));
+            const double wa = __longlong_as_double(((uint64_t)wa2.y << 32) | wa2.x);
+            // image (k0 & 1), pair k0 >> 1, lane's view at dword 2 * lane
+            const uint32_t* rowp = lds + (k0 & 1) * IMG + (r - WID - y0) * RS + (k0 >> 1) * PS;
+            const uint32_t* basep = rowp + 2 * lane;
+            const uint32_t* refl = rowp + 2 * R;
+            uint32_t Sab = 0;
+            if (lane < V) {
+                switch (o) {
+                    case 0: Sab = sab_pairs<WID, 0, RS, PS>(basep, refl, zm); break;
+                    case 1: Sab = sab_pairs<WID, 1, RS, PS>(basep, refl, zm); break;
+                    case 2: Sab = sab_pairs<WID, 2, RS, PS>(basep, refl, zm); break;
+                    default: Sab = sab_pairs<WID, 3, RS, PS>(basep, refl, zm); break;
+                }
+            }
+            // decision: as k_score_tiled3 (see there)
+            const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma_sb, mb.sb));
+            const bool live = lane < V && lane != R && mb.w > 0.0 && wa > 0.0;
+            bool pass = false, guard = false;
+            double ncc = 0.0;
+            if (live) {
+                if (a.thr >= 0.01) {
+                    const double tk = a.thr * (double)(NPX - 1);
+                    const double z = ((double)num * ((double)NPX * wa)) * mb.w;
+                    guard = fabs(z - tk) <= 1e-8 * tk;
+                    pass = z > tk;
+                    ncc = z;
+                } else {
+                    const int32_t db = mom_db(mb);
+                    const int32_t da = mom_db(MomEntry{wa, 0u});
+                    ncc = ((double)num * (double)NPX) /
+                          ((double)(NPX - 1) * sqrt((double)da * (double)db));
+                    guard = fabs(ncc - a.thr) <= kGuard;
+                    pass = ncc > a.thr;
+                    ncc *= (double)(NPX - 1);
+                }
+            }
+            if (__ballot(guard) != 0 && lane == 0) t.fix_list[atomicAdd(t.fix_count, 1)] = cur.x;
+            const uint64_t m = __ballot(pass);
+            const int cnt = __popcll(m);
+            double avgv = 0.0;
+            if (a.avg && cnt)
+                avgv = wave_sum_dpp(pass ? ncc : 0.0) * (c_recip.r[cnt] * (1.0 / (double)(NPX - 1)));
+            const int slot = j - cb;
+            if (lane == 0) {
+                o_mask[slot] = m;
+                o_avg[slot] = avgv;
+                o_cnt[slot] = cnt;
+                o_idx[slot] = cur.x;
+            }
+            cur = nxt;
+            mb_cur = mb_nxt;
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < ce - cb; k += blockDim.x) {
+            const int i = o_idx[k];
+            a.mask[i] = o_mask[k];
+            a.count[i] = o_cnt[k];
+            if (a.avg) a.avg[i] = o_avg[k];
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Tiled scorer for V > 64 (256 views): the views are
 // split into groups of 64 and a work item is (tile chunk, view group).  The
 // workgroup stages the tile's window region of its 64 views only
@@ -2255,6 +2499,26 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
                 case 2: launch_mfma<WID, 2>(sc, a, t, s); break;
                 case 3: launch_mfma<WID, 3>(sc, a, t, s); break;
                 default: launch_mfma<WID, 4>(sc, a, t, s); break;
+            }
+        }
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    if (variant == 11) {
+        // k_score_tiled4 (experimental): 39 % fewer LDS cycles than
+        // k_score_tiled3, same time -- the scorer is not LDS-bound
+        if (sc->mom[WID] == nullptr || sc->V > 64 || (sc->V & 3) != 0 || t->chunk > kChunk ||
+            t->items == nullptr || t->th != kTH || t->tw != kTW)
+            return -3;
+        const size_t outs = (size_t)t->chunk * (8 + 8 + 4 + 4);
+        {
+            TimedLaunch tl(s, ev0, ev1);
+            if (sc->V == 48) {
+                const size_t lds4 = (size_t)2 * G::ROWS * PairGeom<WID>::NP * 2 * 48 * 4 + outs;
+                hipLaunchKernelGGL((k_score_tiled4<WID, 48>), dim3(kTiledBlocks), dim3(kT4Threads), lds4, s, *sc, *a, *t);
+            } else {
+                const size_t lds4 = (size_t)2 * G::ROWS * PairGeom<WID>::NP * 2 * 64 * 4 + outs;
+                hipLaunchKernelGGL((k_score_tiled4<WID, 64>), dim3(kTiledBlocks), dim3(kT4Threads), lds4, s, *sc, *a, *t);
             }
         }
         hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);

@@ -23,20 +23,28 @@ def ctx(pkg, dino):
     c.close()
 
 
-@pytest.fixture(scope="module", params=["direct", "tiled"])
+@pytest.fixture(scope="module", params=["direct", "tiled", "tiled4"])
 def kctx(request, pkg, dino):
-    """A context forced onto one scoring kernel (MVS_SCORE_KERNEL)."""
+    """A context forced onto one scoring kernel (MVS_SCORE_KERNEL; "tiled4" =
+    the tiled path with MVS_VARIANT 11, k_score_tiled4)."""
     import os
     rgb, K, R, t = dino
-    old = os.environ.get("MVS_SCORE_KERNEL")
-    os.environ["MVS_SCORE_KERNEL"] = request.param
+    env = {"MVS_SCORE_KERNEL": "tiled" if request.param == "tiled4" else request.param,
+           "MVS_VARIANT": "11" if request.param == "tiled4" else None}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     try:
         c = pkg.MvsContext(rgb, K, R, t, device=0)
     finally:
-        if old is None:
-            del os.environ["MVS_SCORE_KERNEL"]
-        else:
-            os.environ["MVS_SCORE_KERNEL"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     yield c
     c.close()
 
