@@ -2271,7 +2271,11 @@ __global__ __launch_bounds__(kM2Threads, 3) void k_score_mfma2(const SceneDev sc
 // Re-scores the candidates k_score_tiled3 flagged (a view decision inside the
 // guard band) with the direct scorer, whose guard lanes take the numpy-order
 // ctNcc; overwrites their mask/count/avg.  One wave per flagged candidate.
-constexpr int kFixBlocks = 256;   // one wave per flagged candidate in one round for <= 1024 of them
+// k_score_fix grid: a batch flags a handful of candidates (often none), and
+// the kernel (512 registers per lane, scratch) costs ~28 us per launch over
+// 256 blocks even when its list is empty; 16 blocks = 64 waves in flight.
+// Variant 13 restores the 256-block grid (A/B).
+constexpr int kFixBlocks = 16, kFixBlocksWide = 256;
 
 template <int WID, int NS = 1>
 __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const ScoreArgs a,
@@ -2485,7 +2489,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
                 default: launch_mfma2<WID, 4>(sc, a, t, s); break;
             }
         }
-        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(variant == 13 ? kFixBlocksWide : kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant == 6) {
@@ -2501,7 +2505,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
                 default: launch_mfma<WID, 4>(sc, a, t, s); break;
             }
         }
-        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(variant == 13 ? kFixBlocksWide : kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant == 11) {
@@ -2521,10 +2525,10 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
                 hipLaunchKernelGGL((k_score_tiled4<WID, 64>), dim3(kTiledBlocks), dim3(kT4Threads), lds4, s, *sc, *a, *t);
             }
         }
-        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(variant == 13 ? kFixBlocksWide : kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    if (variant == 4 || variant == 5 || (variant == 0 && sc->mom[WID] != nullptr)) {
+    if (variant == 4 || variant == 5 || variant == 13 || (variant == 0 && sc->mom[WID] != nullptr)) {
         if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kChunk || t->items == nullptr) return -3;
         const size_t outs = (size_t)t->chunk * (8 + 8 + 4 + 4);
         const bool smem = variant == 4;
@@ -2540,7 +2544,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
             else hipLaunchKernelGGL((k_score_tiled3<WID, 64, 0>), dim3(kTiledBlocks), dim3(kT3Threads), lds3, s, *sc, *a, *t);
         }
         }
-        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(variant == 13 ? kFixBlocksWide : kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     TimedLaunch tl(s, ev0, ev1);
