@@ -232,7 +232,16 @@ def main():
                                     "k_score" if a.kernel == "direct" or V % 4 or V > 256 else
                                     "k_score_tiledg"),
                          "kernel_ms": kms, "score_call_ms": pms,
-                         "bytes_per_candidate": B, "candidates_per_launch": n},
+                         "bytes_per_candidate": B, "candidates_per_launch": n,
+                         # measured DRAM bytes (PMC, profiles/pmc_traffic.json) over
+                         # this run's launch time: the HBM bandwidth really drawn
+                         "traffic_GBps": traffic / (kms * 1e-3) / 1e9 if traffic else None,
+                         "traffic_frac": traffic / (kms * 1e-3) / PEAK_HBM if traffic else None,
+                         "note": "achieved counts every candidate's V windows as if read from "
+                                 "HBM; a tile's candidates share them through LDS, so frac can "
+                                 "exceed 1 while traffic_frac is the HBM share actually used; "
+                                 "the kernel is bound by instruction issue/latency, not HBM or "
+                                 "the LDS pipe (DESIGN.md section 6)"},
             "cpu_baseline": cpu,
             "accepted_per_sweep": accepted,
             "gathered_records": gathered["n"],
