@@ -228,7 +228,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM,
                          "traffic": traffic,
-                         "kernel": (KERNEL_NAME[a.kernel] if V <= 64 else
+                         "kernel": ("k_score_tiled5" if V <= 64 and a.wid <= 3 and a.kernel != "direct" else
+                                    KERNEL_NAME[a.kernel] if V <= 64 else
                                     "k_score" if a.kernel == "direct" or V % 4 or V > 256 else
                                     "k_score_tiledg"),
                          "kernel_ms": kms, "score_call_ms": pms,

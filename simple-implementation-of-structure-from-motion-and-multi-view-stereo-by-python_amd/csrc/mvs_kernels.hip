@@ -953,6 +953,67 @@ DEV uint32_t sab_rows(const uint32_t* own_g, const uint32_t* ref_g) {
     return sum;
 }
 
+// Row-streamed S_ab for k_score_tiled5: window rows in groups of RG, the
+// next group's reads issued before the current group's dot products,
+// sched_barriers keeping the compiler from hoisting every read to the front
+// -- 16-32 live window VGPRs instead of 88, so more waves per SIMD fit.
+template <int WID, int O, int RS, int QS>
+DEV uint32_t sab_rows_stream(const uint32_t* own_g, const uint32_t* ref_g) {
+    using M = QuadMasks<WID, O>;
+    constexpr int NB = 2 * WID + 1;
+    // rows per group: pairs (ds_read2st64) while the double buffer stays
+    // small, single rows (ds_read_b32, the same LDS cycles per dword) at wid 5
+    constexpr int RG = M::NQ >= 4 ? 1 : 2;
+    constexpr int NG = (NB + RG - 1) / RG;
+    uint32_t d[2][RG][M::NQ], e[2][RG][M::NQ];
+    lds_u32* ob[M::NQ];
+    lds_u32* rb[M::NQ];
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) {
+        ob[jj] = (lds_u32*)own_g + jj * QS;
+        rb[jj] = (lds_u32*)ref_g + jj * QS;
+        asm volatile("" : "+v"(ob[jj]));
+        asm volatile("" : "+v"(rb[jj]));
+    }
+    auto load = [&](int g, uint32_t (&dd)[RG][M::NQ], uint32_t (&ee)[RG][M::NQ]) {
+#pragma unroll
+        for (int h = 0; h < RG; ++h) {
+            const int row = RG * g + h;
+#pragma unroll
+            for (int jj = 0; jj < M::NQ; ++jj) {
+                dd[h][jj] = row < NB ? ob[jj][row * RS] : 0u;
+                ee[h][jj] = row < NB ? rb[jj][row * RS] : 0u;
+            }
+        }
+    };
+    uint32_t ab[M::NQ];
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) ab[jj] = 0;
+    load(0, d[0], e[0]);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (g + 1 < NG) load(g + 1, d[(g + 1) & 1], e[(g + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < RG; ++h) {
+            if (RG * g + h < NB) {
+#pragma unroll
+                for (int jj = 0; jj < M::NQ; ++jj) {
+                    const uint32_t m = M::mask(jj);
+                    const uint32_t ev = e[g & 1][h][jj];
+                    const uint32_t am = (m == 0xffffffffu) ? ev : (ev & m);
+                    ab[jj] = __builtin_amdgcn_udot4(am, d[g & 1][h][jj], ab[jj], false);
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int jj = 0; jj < M::NQ; ++jj) sum += ab[jj];
+    return sum;
+}
+
 // Same with the reference view's window quads loaded by SMEM (uniform
 // address, s_load) from the view-major copy: no LDS traffic and no VGPRs for
 // the reference side; masks applied on the SALU.
@@ -1145,6 +1206,185 @@ __global__ __launch_bounds__(kT3Threads, 4) void k_score_tiled3(const SceneDev s
                     case 1: Sab = sab_rows_smem<WID, 1, RS, QS>(basep, refg, pitch); break;
                     case 2: Sab = sab_rows_smem<WID, 2, RS, QS>(basep, refg, pitch); break;
                     default: Sab = sab_rows_smem<WID, 3, RS, QS>(basep, refg, pitch); break;
+                }
+            }
+            // num = n S_ab - S_a S_b (|num| < 2^31 for windows up to 11x11: 24-bit
+            // multiplies, exact).  With w = 1/sqrt(n S_bb - S_b^2) per (pixel, view)
+            // from the moments table, ctNcc * (n-1) = n num w_a w_b; it is
+            // compared with thr (n-1).  The three roundings leave < 2e-15 relative
+            // error, so a relative band of 1e-8 around the threshold (far wider
+            // than the reference's own rounding) goes to k_score_fix, which
+            // decides those lanes with the numpy-order ctNcc.
+            static_assert(NPX <= 121, "24-bit moment products need NB <= 11");
+            const int32_t num = (int32_t)(__umul24(NPX, Sab) - __umul24(ma_sb, mb.sb));
+            const bool live = lane < V && lane != R && mb.w > 0.0 && wa > 0.0;
+            bool pass = false, guard = false;
+            double ncc = 0.0;
+            if (live) {
+                if (a.thr >= 0.01) {
+                    const double tk = a.thr * (double)(NPX - 1);
+                    const double z = ((double)num * ((double)NPX * wa)) * mb.w;   // ncc (n-1)
+                    guard = fabs(z - tk) <= 1e-8 * tk;
+                    pass = z > tk;
+                    ncc = z;
+                } else {
+                    // the reference view's n S_aa - S_a^2 from its (wave-uniform) w: lane R
+                    // itself is not live, so its lane value cannot be read back here
+                    const int32_t db = mom_db(mb);
+                    const int32_t da = mom_db(MomEntry{wa, 0u});
+                    ncc = ((double)num * (double)NPX) /
+                          ((double)(NPX - 1) * sqrt((double)da * (double)db));
+                    guard = fabs(ncc - a.thr) <= kGuard;
+                    pass = ncc > a.thr;
+                    ncc *= (double)(NPX - 1);
+                }
+            }
+            if (__ballot(guard) != 0 && lane == 0) t.fix_list[atomicAdd(t.fix_count, 1)] = cur.x;
+            const uint64_t m = __ballot(pass);
+            const int cnt = __popcll(m);
+            double avgv = 0.0;
+            if (a.avg && cnt)
+                avgv = wave_sum_dpp(pass ? ncc : 0.0) * (c_recip.r[cnt] * (1.0 / (double)(NPX - 1)));
+            const int slot = j - cb;
+            if (lane == 0) {
+                o_mask[slot] = m;
+                o_avg[slot] = avgv;
+                o_cnt[slot] = cnt;
+                o_idx[slot] = cur.x;
+            }
+            cur = nxt;
+            mb_cur = mb_nxt;
+        }
+        __syncthreads();
+        STAMP(2);
+        for (int k = threadIdx.x; k < ce - cb; k += blockDim.x) {
+            const int i = o_idx[k];
+            a.mask[i] = o_mask[k];
+            a.count[i] = o_cnt[k];
+            if (a.avg) a.avg[i] = o_avg[k];
+        }
+        __syncthreads();
+        STAMP(3);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Tiled scorer v5 (default for wid <= 3; variants 14/15): k_score_tiled3 with 8-wave
+// workgroups and row-streamed window reads (sab_rows_stream), so that VGPRs
+// (and, at 34 KB of LDS per workgroup, 4 workgroups per CU) allow OCC waves
+// per SIMD instead of 4.
+constexpr int kT5Threads = 512, kT5Waves = kT5Threads / 64;
+
+template <int WID, int QS, int OCC>
+__global__ __launch_bounds__(kT5Threads, OCC) void k_score_tiled5(const SceneDev sc, const ScoreArgs a,
+                                                                const TiledArgs t) {
+    using G = TileGeom<WID>;
+    constexpr int NB = 2 * WID + 1;
+    constexpr int NPX = NB * NB;
+    // QS: dwords per (row, quad) slot of the LDS image (= V when V == 48)
+    constexpr int RS = G::NQ * QS;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int V = sc.V;
+    const int n_items = t.item_off[t.ntiles];
+    // wave index as an SGPR: the candidate loop, its SMEM loads and the
+    // alignment switch below are then scalar control flow
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const MomEntry* __restrict__ mom = sc.mom[WID];
+    // output staging behind the region image (chunk <= kChunk candidates)
+    uint64_t* o_mask = (uint64_t*)(lds + G::ROWS * RS);
+    double* o_avg = (double*)(o_mask + t.chunk);
+    int32_t* o_cnt = (int32_t*)(o_avg + t.chunk);
+    int32_t* o_idx = o_cnt + t.chunk;
+    __shared__ int s_item;
+#ifdef MVS_STAMPS
+    unsigned long long st_prev = 0;
+#endif
+    for (;;) {
+        // dynamic work queue: the next (tile, chunk) item for this workgroup
+        if (threadIdx.x == 0) s_item = atomicAdd(&t.tile_count[t.ntiles], 1);
+        __syncthreads();
+        // uniform from here on: tile bounds and offsets live in SGPRs
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item >= n_items) break;
+        STAMP(0);
+        // longest-first item list (k_tile_scan); uniform address -> scalar load
+        const unsigned long long itv =
+            *(const __attribute__((address_space(4))) unsigned long long*)(t.items + item);
+        const int tile = (int)(uint32_t)itv, chunk = (int)(uint32_t)(itv >> 32);
+        const int cb = t.tile_off[tile] + chunk * t.chunk;
+        const int ce = min(cb + t.chunk, t.tile_off[tile + 1]);
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int y0 = ty * kTH - WID;
+        const int kq0 = tx * (kTW / 4) + G::KQ0;
+        {
+            const int cpq = V >> 2, cpr = G::NQ * cpq, total = G::ROWS * cpr;
+            for (int base = 0; base < total; base += 2 * kT5Threads) {
+                uint4 buf[2];
+                int dst[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int k = base + u * kT5Threads + (int)threadIdx.x;
+                    dst[u] = -1;
+                    buf[u] = make_uint4(0, 0, 0, 0);
+                    if (k < total) {
+                        const int ry = k / cpr, rem = k - ry * cpr;
+                        const int kq = rem / cpq, vq = rem - kq * cpq;
+                        const int y = y0 + ry, gq = kq0 + kq;
+                        if (y >= 0 && y < sc.H && gq >= 0 && gq < sc.Wq)
+                            buf[u] = *(const uint4*)(sc.stack + (int64_t)y * sc.row_bytes +
+                                                      (int64_t)gq * V * 4 + vq * 16);
+                        dst[u] = (ry * G::NQ + kq) * QS + vq * 4;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    if (dst[u] >= 0) *(uint4*)(lds + dst[u]) = buf[u];
+            }
+        }
+        __syncthreads();
+        STAMP(1);
+        // Candidates: outputs go to an LDS staging slot and leave the CU after
+        // the loop, so no wave ever waits on its own stores (vmcnt counts
+        // stores and loads together, in order).  The next candidate's entry
+        // (SMEM) and moments (VMEM) are fetched one iteration ahead.
+        auto sload = [](const int2* p) -> int2 {   // uniform address -> s_load_dwordx2
+            const unsigned long long v = *(const __attribute__((address_space(4))) unsigned long long*)p;
+            return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+        };
+        int2 cur = cb + wave < ce ? sload(t.sorted + cb + wave) : make_int2(0, 0);
+        MomEntry mb_cur{0.0, 0u};
+        if (cb + wave < ce) {
+            const int pk = cur.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
+            if (lane < V) mb_cur = load_mom(mom, (r * sc.W + q) * V + lane);
+        }
+        for (int j = cb + wave; j < ce; j += kT5Waves) {
+            const int2 nxt = j + kT5Waves < ce ? sload(t.sorted + j + kT5Waves) : make_int2(0, 0);
+            MomEntry mb_nxt{0.0, 0u};
+            if (j + kT5Waves < ce) {
+                const int pk = nxt.y, q = pk & 0x7ff, r = (pk >> 11) & 0x7ff;
+                if (lane < V) mb_nxt = load_mom(mom, (r * sc.W + q) * V + lane);
+            }
+            const int pk = cur.y;
+            const int q = pk & 0x7ff, r = (pk >> 11) & 0x7ff, R = (pk >> 22) & 0x3ff;
+            const int q0 = q - WID, o = q0 & 3;
+            const int k0 = (q0 >> 2) - kq0;
+            const MomEntry mb = mb_cur;
+            // the reference view's moments: lane R's entry
+            const uint32_t ma_sb = __builtin_amdgcn_readlane(mb.sb, R);
+            const uint2 wa2 = make_uint2(__builtin_amdgcn_readlane((uint32_t)__double_as_longlong(mb.w), R),
+                                         __builtin_amdgcn_readlane((uint32_t)((uint64_t)__double_as_longlong(mb.w) >> 32), R));
+            const double wa = __longlong_as_double(((uint64_t)wa2.y << 32) | wa2.x);
+            const uint32_t* basep = lds + (r - WID - y0) * RS + k0 * QS + lane;
+            // the reference view's quads: same LDS address in every lane (broadcast)
+            const uint32_t* refl = basep - lane + R;
+            uint32_t Sab = 0;
+            if (lane < V) {
+                switch (o) {
+                    case 0: Sab = sab_rows_stream<WID, 0, RS, QS>(basep, refl); break;
+                    case 1: Sab = sab_rows_stream<WID, 1, RS, QS>(basep, refl); break;
+                    case 2: Sab = sab_rows_stream<WID, 2, RS, QS>(basep, refl); break;
+                    default: Sab = sab_rows_stream<WID, 3, RS, QS>(basep, refl); break;
                 }
             }
             // num = n S_ab - S_a S_b (|num| < 2^31 for windows up to 11x11: 24-bit
@@ -2526,6 +2766,30 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
             }
         }
         hipLaunchKernelGGL(k_score_fix<WID>, dim3(variant == 13 ? kFixBlocksWide : kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    // default for windows up to 7x7: k_score_tiled5 at 8 waves/SIMD (fits 64
+    // VGPRs there; at wid 4-5 it spills and k_score_tiled3 stays)
+    if (variant == 0 && WID <= 3 && sc->mom[WID] != nullptr && sc->V <= 64 && (sc->V & 3) == 0 &&
+        t->chunk <= kChunk && t->items != nullptr)
+        variant = 15;
+    if (variant == 14 || variant == 15) {
+        if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || sc->V > 64 || t->chunk > kChunk || t->items == nullptr)
+            return -3;
+        const size_t outs = (size_t)t->chunk * (8 + 8 + 4 + 4);
+        {
+            TimedLaunch tl(s, ev0, ev1);
+            if (sc->V == 48) {
+                const size_t lds3 = (size_t)G::ROWS * G::NQ * 48 * 4 + outs;
+                if (variant == 14) hipLaunchKernelGGL((k_score_tiled5<WID, 48, 6>), dim3(kTiledBlocks), dim3(kT5Threads), lds3, s, *sc, *a, *t);
+                else hipLaunchKernelGGL((k_score_tiled5<WID, 48, 8>), dim3(kTiledBlocks), dim3(kT5Threads), lds3, s, *sc, *a, *t);
+            } else {
+                const size_t lds3 = (size_t)G::ROWS * G::NQ * 64 * 4 + outs;
+                if (variant == 14) hipLaunchKernelGGL((k_score_tiled5<WID, 64, 6>), dim3(kTiledBlocks), dim3(kT5Threads), lds3, s, *sc, *a, *t);
+                else hipLaunchKernelGGL((k_score_tiled5<WID, 64, 8>), dim3(kTiledBlocks), dim3(kT5Threads), lds3, s, *sc, *a, *t);
+            }
+        }
+        hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant == 4 || variant == 5 || variant == 13 || (variant == 0 && sc->mom[WID] != nullptr)) {

@@ -1,3 +1,5 @@
+#!/bin/bash
+# GPU parity tests only.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -x -q -m gpu ${1:+-k "$1"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -15 gpurun_out/pytest_gpu.log; exit $rc
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; exit $rc
