@@ -954,9 +954,10 @@ DEV uint32_t sab_rows(const uint32_t* own_g, const uint32_t* ref_g) {
 }
 
 // Row-streamed S_ab for k_score_tiled5: window rows in groups of RG, the
-// next group's reads issued before the current group's dot products,
-// sched_barriers keeping the compiler from hoisting every read to the front
-// -- 16-32 live window VGPRs instead of 88, so more waves per SIMD fit.
+// next group's reads issued before the current group's dot products, an
+// empty asm tying their addresses to the accumulators keeping the compiler
+// from hoisting every read to the front -- 16-32 live window VGPRs instead of
+// 88, so more waves per SIMD fit.
 template <int WID, int O, int RS, int QS>
 DEV uint32_t sab_rows_stream(const uint32_t* own_g, const uint32_t* ref_g) {
     using M = QuadMasks<WID, O>;
@@ -966,23 +967,16 @@ DEV uint32_t sab_rows_stream(const uint32_t* own_g, const uint32_t* ref_g) {
     constexpr int RG = M::NQ >= 4 ? 1 : 2;
     constexpr int NG = (NB + RG - 1) / RG;
     uint32_t d[2][RG][M::NQ], e[2][RG][M::NQ];
-    lds_u32* ob[M::NQ];
-    lds_u32* rb[M::NQ];
-#pragma unroll
-    for (int jj = 0; jj < M::NQ; ++jj) {
-        ob[jj] = (lds_u32*)own_g + jj * QS;
-        rb[jj] = (lds_u32*)ref_g + jj * QS;
-        asm volatile("" : "+v"(ob[jj]));
-        asm volatile("" : "+v"(rb[jj]));
-    }
+    lds_u32* ob = (lds_u32*)own_g;
+    lds_u32* rb = (lds_u32*)ref_g;
     auto load = [&](int g, uint32_t (&dd)[RG][M::NQ], uint32_t (&ee)[RG][M::NQ]) {
 #pragma unroll
         for (int h = 0; h < RG; ++h) {
             const int row = RG * g + h;
 #pragma unroll
             for (int jj = 0; jj < M::NQ; ++jj) {
-                dd[h][jj] = row < NB ? ob[jj][row * RS] : 0u;
-                ee[h][jj] = row < NB ? rb[jj][row * RS] : 0u;
+                dd[h][jj] = row < NB ? ob[row * RS + jj * QS] : 0u;
+                ee[h][jj] = row < NB ? rb[row * RS + jj * QS] : 0u;
             }
         }
     };
@@ -992,8 +986,13 @@ DEV uint32_t sab_rows_stream(const uint32_t* own_g, const uint32_t* ref_g) {
     load(0, d[0], e[0]);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-        if (g + 1 < NG) load(g + 1, d[(g + 1) & 1], e[(g + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
+        if (g + 1 < NG) {
+            // the next group's addresses "depend" on the accumulators as they
+            // stand after group g-1: its reads cannot be hoisted further up, so
+            // at most two groups of window words are live
+            asm volatile("" : "+v"(ob), "+v"(rb) : "v"(ab[0]));
+            load(g + 1, d[(g + 1) & 1], e[(g + 1) & 1]);
+        }
 #pragma unroll
         for (int h = 0; h < RG; ++h) {
             if (RG * g + h < NB) {
@@ -1006,7 +1005,6 @@ DEV uint32_t sab_rows_stream(const uint32_t* own_g, const uint32_t* ref_g) {
                 }
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
     uint32_t sum = 0;
 #pragma unroll
@@ -2792,7 +2790,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         hipLaunchKernelGGL(k_score_fix<WID>, dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    if (variant == 4 || variant == 5 || variant == 13 || (variant == 0 && sc->mom[WID] != nullptr)) {
+    if (variant == 4 || variant == 5 || variant == 10 || variant == 13 || (variant == 0 && sc->mom[WID] != nullptr)) {
         if (sc->mom[WID] == nullptr || (sc->V & 3) != 0 || t->chunk > kChunk || t->items == nullptr) return -3;
         const size_t outs = (size_t)t->chunk * (8 + 8 + 4 + 4);
         const bool smem = variant == 4;
