@@ -27,7 +27,7 @@ PKG_NAME = "simple-implementation-of-structure-from-motion-and-multi-view-stereo
 sys.path.insert(0, REPO)
 
 PEAK_HBM = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
-KERNEL_NAME = {"auto": "k_score_tiled3", "tiled": "k_score_tiled3", "direct": "k_score"}
+KERNEL_NAME = {"auto": "k_score_tiled3", "tiled": "k_score_tiled3", "direct": "k_score"}  # variant 10 A/B only; the default is k_score_tiled5
 
 
 def algorithmic_bytes(V, wid):
@@ -228,7 +228,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM,
                          "traffic": traffic,
-                         "kernel": ("k_score_tiled5" if V <= 64 and a.wid <= 3 and a.kernel != "direct" else
+                         "kernel": ("k_score_tiled5" if V <= 64 and a.kernel != "direct" else
                                     KERNEL_NAME[a.kernel] if V <= 64 else
                                     "k_score" if a.kernel == "direct" or V % 4 or V > 256 else
                                     "k_score_tiledg"),

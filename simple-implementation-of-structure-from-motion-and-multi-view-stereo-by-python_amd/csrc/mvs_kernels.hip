@@ -989,7 +989,12 @@ DEV uint32_t sab_rows_stream(const uint32_t* own_g, const uint32_t* ref_g) {
         if (g + 1 < NG) {
             // the next group's addresses "depend" on the accumulators as they
             // stand after group g-1: its reads cannot be hoisted further up, so
-            // at most two groups of window words are live
+            // at most two groups of window words are live; pinning every
+            // accumulator (not only ab[0]) also stops the scheduler from
+            // sinking the group-g ALU work below the next loads (12 VGPR
+            // spills at wid 5 without it, none with it)
+#pragma unroll
+            for (int jj = 0; jj < M::NQ; ++jj) asm volatile("" : "+v"(ab[jj]));
             asm volatile("" : "+v"(ob), "+v"(rb) : "v"(ab[0]));
             load(g + 1, d[(g + 1) & 1], e[(g + 1) & 1]);
         }
@@ -2766,9 +2771,10 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         hipLaunchKernelGGL(k_score_fix<WID>, dim3(variant == 13 ? kFixBlocksWide : kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    // default for windows up to 7x7: k_score_tiled5 at 8 waves/SIMD (fits 64
-    // VGPRs there; at wid 4-5 it spills and k_score_tiled3 stays)
-    if (variant == 0 && WID <= 3 && sc->mom[WID] != nullptr && sc->V <= 64 && (sc->V & 3) == 0 &&
+    // default for every window size: k_score_tiled5 at 8 waves/SIMD (64
+    // VGPRs; wid 5 0.417 vs 0.426 ms for tiled3, profiles/r01/ab_tiled5_pin_w5.log;
+    // wid 4 0.339 vs 0.373 ms despite 4 spilled VGPRs, ab_tiled5_pin_w4.log)
+    if (variant == 0 && sc->mom[WID] != nullptr && sc->V <= 64 && (sc->V & 3) == 0 &&
         t->chunk <= kChunk && t->items != nullptr)
         variant = 15;
     if (variant == 14 || variant == 15) {

@@ -23,14 +23,15 @@ def ctx(pkg, dino):
     c.close()
 
 
-@pytest.fixture(scope="module", params=["direct", "tiled", "tiled4", "tiled5"])
+@pytest.fixture(scope="module", params=["direct", "tiled", "tiled3", "tiled4", "tiled5"])
 def kctx(request, pkg, dino):
-    """A context forced onto one scoring kernel (MVS_SCORE_KERNEL; "tiled4" /
-    "tiled5" = the tiled path with MVS_VARIANT 11 / 15: the experimental
-    k_score_tiled4 / k_score_tiled5)."""
+    """A context forced onto one scoring kernel (MVS_SCORE_KERNEL; "tiled3" /
+    "tiled4" / "tiled5" = the tiled path with MVS_VARIANT 10 / 11 / 15:
+    k_score_tiled3, the experimental k_score_tiled4, k_score_tiled5 — the
+    default "tiled" path is k_score_tiled5 too)."""
     import os
     rgb, K, R, t = dino
-    variant = {"tiled4": "11", "tiled5": "15"}.get(request.param)
+    variant = {"tiled3": "10", "tiled4": "11", "tiled5": "15"}.get(request.param)
     env = {"MVS_SCORE_KERNEL": "tiled" if variant else request.param, "MVS_VARIANT": variant}
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
