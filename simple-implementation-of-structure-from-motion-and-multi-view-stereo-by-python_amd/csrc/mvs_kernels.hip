@@ -17,6 +17,7 @@
 // with -ffp-contract=off (products that numpy/OpenBLAS fuse are written as
 // fma() explicitly).
 #include <algorithm>
+#include <cstdlib>
 
 #include "mvs_internal.h"
 
@@ -580,8 +581,9 @@ struct TileGeom {
 // and rank it inside its tile.  Ranks come from an LDS histogram per block
 // (one global atomic per non-empty (block, tile) pair), not from a global
 // atomic per candidate.
-constexpr int kBinBlock = 1024, kBinPer = 4;
+constexpr int kBinBlock = 1024, kBinPerDefault = 4;
 
+template <int kBinPer>
 __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t, int wid) {
     extern __shared__ int32_t hist[];      // [ntiles] local counts, then global bases
@@ -626,6 +628,30 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         if (tl[k] < 0) continue;
         t.cand_key[i] = tl[k];
         t.cand_rank[i] = hist[tl[k]] + lr[k];
+    }
+}
+
+// candidates per k_bin thread (MVS_BIN_PER = 1/2/4/8, read once; A/B only):
+// fewer per thread = more blocks, but one more global atomic per (block, tile)
+static int bin_per() {
+    static const int p = [] {
+        const char* e = getenv("MVS_BIN_PER");
+        const int v = e ? atoi(e) : kBinPerDefault;
+        return (v == 1 || v == 2 || v == 4 || v == 8) ? v : kBinPerDefault;
+    }();
+    return p;
+}
+
+static void launch_bin(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid, hipStream_t s) {
+    const int per = bin_per();
+    const int64_t per_block = (int64_t)kBinBlock * per;
+    const int nbin = (int)((a->n + per_block - 1) / per_block);
+    const size_t lds = (size_t)t->ntiles * 4;
+    switch (per) {
+        case 1: hipLaunchKernelGGL(k_bin<1>, dim3(nbin), dim3(kBinBlock), lds, s, *sc, *a, *t, wid); break;
+        case 2: hipLaunchKernelGGL(k_bin<2>, dim3(nbin), dim3(kBinBlock), lds, s, *sc, *a, *t, wid); break;
+        case 8: hipLaunchKernelGGL(k_bin<8>, dim3(nbin), dim3(kBinBlock), lds, s, *sc, *a, *t, wid); break;
+        default: hipLaunchKernelGGL(k_bin<4>, dim3(nbin), dim3(kBinBlock), lds, s, *sc, *a, *t, wid); break;
     }
 }
 
@@ -2712,9 +2738,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     if (t->zero_first &&
         hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess)
         return -1;
-    const int64_t per_block = (int64_t)kBinBlock * kBinPer;
-    const int nbin = (int)((a->n + per_block - 1) / per_block);
-    hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
+    launch_bin(sc, a, t, WID, s);
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, *t);
     const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
@@ -2841,9 +2865,7 @@ int launch_score_tiledg_w(const SceneDev* sc, const ScoreArgs* a, const TiledArg
         (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess ||
          hipMemsetAsync(t->xq, 0, sizeof(int32_t) * 8, s) != hipSuccess))
         return -1;
-    const int64_t per_block = (int64_t)kBinBlock * kBinPer;
-    const int nbin = (int)((a->n + per_block - 1) / per_block);
-    hipLaunchKernelGGL(k_bin, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
+    launch_bin(sc, a, t, WID, s);
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, *t);
     const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
