@@ -47,7 +47,7 @@ const char* mvs_version(void);
  * device gray stack (OpenCV BGR2GRAY fixed-point formula applied to the RGB
  * data, as the reference does) and the per-view camera table.
  * Rp may be NULL (the library computes R' = Rodrigues(Rodrigues(R))).
- * V <= 256, H, W >= 16. */
+ * 1 <= V <= 256, 16 <= H, W <= 65536. */
 int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const double* K,
                    const double* R, const double* t, const double* Rp, mvs_ctx** out);
 void mvs_ctx_destroy(mvs_ctx* ctx);
@@ -68,6 +68,8 @@ int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp);
 int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int wid,
               double min_ncc, double* xy, uint64_t* mask, int32_t* count, double* avg);
 /* Same on device pointers (e.g. torch tensor data_ptr()), stream-ordered.
+ * Calls on different streams are ordered too: a call waits for the previous
+ * call's use of the context's scratch (an event on that call's stream).
  * d_avg may be NULL when avg_ncc_score is not needed (it only feeds the
  * disabled filter_out_outlier, MVS2.py:281). */
 int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
@@ -75,12 +77,14 @@ int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* 
                      double* d_avg, void* stream);
 /* Kernel timing (measurement only): while enabled, every scoring call records a
  * HIP event pair on its stream immediately around the dominant scoring kernel
- * (k_score_tiled3, or k_score for small/large-V batches).  enable != 0 resets
- * the record and turns it on; 0 turns it off (the record stays readable).
- * mvs_kernel_time synchronises the recorded events and returns the summed
- * kernel time and the number of timed launches. */
+ * (k_score_mma for batches of >= 2048 candidates, else k_score).  enable != 0
+ * resets the record and turns it on; 0 turns it off (the record stays
+ * readable).  mvs_kernel_time synchronises the recorded events and returns
+ * the summed kernel time and the number of timed launches; mvs_timed_kernel
+ * names the kernel the last recorded pair bracketed. */
 int mvs_kernel_timing(mvs_ctx* ctx, int enable);
 int mvs_kernel_time(mvs_ctx* ctx, double* total_ms, int64_t* launches);
+const char* mvs_timed_kernel(const mvs_ctx* ctx);
 /* Number of per-view NCC decisions that fell inside the guard band around the
  * threshold (relative 1e-8 on the squared comparison; 1e-9 absolute when
  * min_ncc < 0.01) and were re-evaluated in numpy order since the context was

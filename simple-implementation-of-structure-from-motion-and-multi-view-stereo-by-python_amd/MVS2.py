@@ -10,6 +10,7 @@ MyPatch.photo_consistenecy_test(...)          MVS2.py:62-77
     scorer.  Use photo_consistency_batch for many candidates.
 """
 import time
+import zlib
 
 import numpy as np
 
@@ -25,15 +26,39 @@ def _device_index():
     return int(os.environ.get("LOCAL_RANK", os.environ.get("MVS_DEVICE", "0")))
 
 
+def _images_key(imgs):
+    """Identity and a content fingerprint of the image list: the element
+    arrays' ids, buffers and shapes, and a CRC of every 61st row of each image.
+    The reference re-reads imgs on every photo test; a caller that replaces an
+    array, or rewrites any sampled row in place, gets a fresh context.  (A
+    change confined to unsampled rows is not seen: call clear_context_cache().)"""
+    parts = [id(imgs), len(imgs)]
+    crc = 0
+    for a in imgs:
+        a = np.asarray(a)
+        parts += [id(a), a.shape, a.__array_interface__["data"][0]]
+        crc = zlib.crc32(np.ascontiguousarray(a[::61]).tobytes(), crc)
+    parts.append(crc)
+    return tuple(parts)
+
+
+def clear_context_cache():
+    """Drop the cached GPU context (e.g. after editing images in place)."""
+    for ctx, _ in _ctx_cache.values():
+        ctx.close()
+    _ctx_cache.clear()
+
+
 def scene_context(imgs, par_K, par_r, par_t, device=None):
-    """MvsContext for (imgs, cameras), cached on the identity of imgs and the
-    camera values (SfM and MVS each call read_pars, MVS2.py:178 / SFM.py:54)."""
+    """MvsContext for (imgs, cameras), cached on the images (identity + a
+    sampled content fingerprint, _images_key) and the camera values (SfM and
+    MVS each call read_pars, MVS2.py:178 / SFM.py:54)."""
     K, R, t = pars_to_arrays(par_K, par_r, par_t, len(imgs))
-    key = (id(imgs), len(imgs), K.tobytes(), R.tobytes(), t.tobytes())
+    key = (_images_key(imgs), K.tobytes(), R.tobytes(), t.tobytes())
     ctx = _ctx_cache.get(key)
     if ctx is None:
         ctx = _lib.MvsContext(imgs, K, R, t, device=_device_index() if device is None else device)
-        _ctx_cache.clear()
+        clear_context_cache()
         _ctx_cache[key] = (ctx, imgs)
         return ctx
     return ctx[0]

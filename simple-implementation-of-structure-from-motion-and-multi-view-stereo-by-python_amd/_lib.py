@@ -36,6 +36,7 @@ SIGNATURES = [
     ("mvs_kernel_timing", ctypes.c_int, [_vp, ctypes.c_int]),
     ("mvs_kernel_time", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_int64)]),
+    ("mvs_timed_kernel", ctypes.c_char_p, [_vp]),
     ("mvs_ncc_windows", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_double,
                                        ctypes.c_int, _vp, _vp, _vp]),
     ("mvs_stage_run", ctypes.c_int, [_vp, ctypes.c_int64, _i64p, _i32p, _fp, ctypes.c_int,
@@ -218,6 +219,11 @@ class MvsContext:
         check(load().mvs_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(k)), self._h,
               "mvs_kernel_time")
         return ms.value, int(k.value)
+
+    def timed_kernel(self):
+        """Name of the kernel the last timed event pair bracketed."""
+        name = load().mvs_timed_kernel(self._h)
+        return name.decode() if name else ""
 
     def score(self, c, ref, min_ncc=0.7, wid=5):
         """Batched photo_consistenecy_test (MVS2.py:62-77) on host arrays.

@@ -12,8 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmvs_amd.so")
 STAMPS_LIB = os.path.join(HERE, "libmvs_amd_stamps.so")   # diagnostic build (-DMVS_STAMPS)
-SOURCES = ["mvs_kernels.hip", "mvs_engine.cpp"]
-HEADERS = ["mvs_internal.h", os.path.join("..", "..", "include", "mvs_amd.h")]
+SOURCES = ["mvs_kernels.hip", "sfm_kernels.hip", "mvs_engine.cpp"]
+HEADERS = ["mvs_internal.h", "mvs_device.h", os.path.join("..", "..", "include", "mvs_amd.h")]
 ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
 
 

@@ -297,7 +297,6 @@ struct mvs_ctx {
     std::vector<double> K;   // V*9 as given (getProjectionMatrix uses all of K)
     std::vector<uint8_t> h_rgb;
     DevBuf<uint8_t> d_rgb, d_stack, d_gv;
-    DevBuf<MomEntry> d_mom[MVS_MAX_WID + 1];
     DevBuf<CamDev> d_cams;
     DevBuf<int32_t> d_exact;
     SceneDev sc{};
@@ -314,14 +313,26 @@ struct mvs_ctx {
     DevBuf<uint32_t> f_key, f_desc;
     DevBuf<int32_t> f_rows, f_pts, f_mom, f_best;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
-    int variant = 0;       // tiled-kernel variant (env MVS_VARIANT), see mvs_kernels.hip
-    int chunk3 = 256;      // candidates per work item of the v3 tiled kernel (env MVS_TILE_CHUNK)
     int tiles_clean_ntiles = -1;   // tile counters known zero for this tile count (-1: unknown)
     // kernel timing (mvs_kernel_timing): one event pair per scoring launch
     bool timing = false;
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
+    const char* timed_name = "";   // the kernel the last timed pair bracketed
+    // The context's scratch (tiled-scorer counters and lists, host-pointer
+    // buffers) may be used on any stream a *_device call names: every use
+    // waits for the previous one (an event on the stream that used it last).
+    hipEvent_t scratch_ev = nullptr;
+    hipStream_t scratch_s = nullptr;
     std::string err;
+    void scratch_acquire(hipStream_t s) {
+        if (scratch_s && scratch_s != s) HIPCHK(hipStreamWaitEvent(s, scratch_ev, 0));
+    }
+    void scratch_release(hipStream_t s) {
+        if (!scratch_ev) HIPCHK(hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(scratch_ev, s));
+        scratch_s = s;
+    }
     // next event pair while timing is on, else nulls
     void next_events(hipEvent_t* e0, hipEvent_t* e1) {
         *e0 = *e1 = nullptr;
@@ -414,34 +425,24 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
     a.count = d_count;
     a.avg = d_avg;
     a.exact_hits = ctx->d_exact.p;
-    // tiled scorers: k_score_tiled3 (V <= 64) and the view-group k_score_tiledg
-    // (64 < V <= 256, V a multiple of 4); the direct k_score takes the rest and
-    // small batches
-    const bool grouped = ctx->V > 64;
-    const bool tiled_ok = !grouped || ((ctx->V & 3) == 0 && ctx->V <= 256);
-    const bool tiled = tiled_ok && (ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048));
-    // the MFMA scorer stages 16-B groups of 4 views: other view counts take the 16x8 tiled path
-    const int variant = grouped || ((ctx->variant == 6 || ctx->variant == 9) && (ctx->V & 3) != 0) ? 0 : ctx->variant;
-    if (tiled && (grouped || variant == 0 || variant >= 4) && (ctx->V & 3) == 0 &&
-        !ctx->sc.mom[wid]) {
-        // scene moments for this window size: built once, reused by every batch
-        ctx->d_mom[wid].alloc((size_t)ctx->H * ctx->W * ctx->V);
-        if (mvs_launch_build_moments(&ctx->sc, wid, ctx->d_mom[wid].p, s) != 0)
-            throw Fail{MVS_E_HIP, "moments launch failed"};
-        ctx->sc.mom[wid] = ctx->d_mom[wid].p;
-    }
+    // the tiled matrix-core scorer (k_score_mma, any V <= 256) for batches of
+    // >= 2048 candidates; the direct k_score for small batches
+    const bool grouped = ctx->V > MVS_GROUP_VIEWS;
+    const bool tiled = ctx->kernel_mode == 2 || (ctx->kernel_mode == 0 && n >= 2048);
     if (tiled) {
-        const bool mfma = variant == 6;
         TiledArgs t{};
-        mvs_tiled_geometry(ctx->W, ctx->H, mfma ? 1 : 0, &t.tw, &t.th, &t.ntx, &t.nty);
+        t.tw = MVS_TILE_W;
+        t.th = MVS_TILE_H;
+        t.ntx = (ctx->W + MVS_TILE_W - 1) / MVS_TILE_W;
+        t.nty = (ctx->H + MVS_TILE_H - 1) / MVS_TILE_H;
         const int ntiles = t.ntx * t.nty;
         const int32_t* tiles_before = ctx->t_tiles.p;
         ctx->t_tiles.ensure((size_t)3 * (ntiles + 2) + 8);
         if (ctx->t_tiles.p != tiles_before) ctx->tiles_clean_ntiles = -1;
-        const int groups = grouped ? (ctx->V + 63) / 64 : 1;
+        const int groups = grouped ? (ctx->V + MVS_GROUP_VIEWS - 1) / MVS_GROUP_VIEWS : 1;
         ctx->t_cand.ensure((size_t)(5 + groups) * n);   // fix_list: one entry per (candidate, group)
         t.ntiles = ntiles;
-        t.chunk = grouped ? ctx->chunk3 : mfma ? 1024 : variant == 9 ? 256 : (variant == 0 || variant >= 4) ? ctx->chunk3 : 512;
+        t.chunk = grouped ? MVS_GROUP_CHUNK : MVS_MMA_CHUNK;
         t.groups = groups;
         if (grouped) {
             ctx->t_pcnt.ensure((size_t)groups * n);
@@ -458,7 +459,6 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.cand_pk = ctx->t_cand.p + 2 * n;
         t.sorted = (int2*)(ctx->t_cand.p + 3 * n);
         t.fix_list = ctx->t_cand.p + 5 * n;
-        t.xq = ctx->t_tiles.p + 3 * (ntiles + 2);
         // at most one partial chunk per tile beyond the full ones
         ctx->t_items.ensure((size_t)(n / std::max(t.chunk, 1) + ntiles + 2));
         t.items = ctx->t_items.p;
@@ -466,14 +466,36 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         ctx->tiles_clean_ntiles = -1;            // dirty until the sequence is queued
         hipEvent_t e0, e1;
         ctx->next_events(&e0, &e1);
-        if (mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, variant, s, e0, e1) != 0)
-            throw Fail{MVS_E_HIP, "tiled score launch failed"};
+        ctx->scratch_acquire(s);
+        const int rc = mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, s, e0, e1);
+        if (rc != 0) throw Fail{rc == -3 ? MVS_E_UNSUPPORTED : MVS_E_HIP, "tiled score launch failed"};
+        ctx->scratch_release(s);
+        if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, 1);
         ctx->tiles_clean_ntiles = ntiles;        // k_tile_scan leaves the counters zero
         return;
     }
     hipEvent_t e0, e1;
     ctx->next_events(&e0, &e1);
     if (mvs_launch_score(&ctx->sc, &a, wid, s, e0, e1) != 0) throw Fail{MVS_E_HIP, "score launch failed"};
+    if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, 0);
+}
+
+// patch_expansion children (MVS2.py:329-369) of a.n jobs into records
+// a.first_out + [0, a.n): small batches one wave per child (k_expand), large
+// ones as child geometry, the children's photo test on the tiled matrix-core
+// scorer, then the accept test
+void expand_device(mvs_ctx* ctx, const RecordsDev& r, const ExpandArgs& a, int wid, hipStream_t s) {
+    if (a.n <= 0) return;
+    if (ctx->kernel_mode == 1 || a.n < 2048) {
+        if (mvs_launch_expand(&ctx->sc, r, &a, wid, s) != 0) throw Fail{MVS_E_HIP, "expand launch failed"};
+        return;
+    }
+    const int64_t f = a.first_out;
+    const int words = ctx->words();
+    if (mvs_launch_expand_geom(&ctx->sc, r, &a, s) != 0) throw Fail{MVS_E_HIP, "expand_geom launch failed"};
+    score_device(ctx, a.n, r.c + 3 * f, r.R + f, wid, a.thr, r.xy + 2 * f, r.mask + words * f, r.count + f,
+                 nullptr, s);
+    if (mvs_launch_expand_accept(r, &a, s) != 0) throw Fail{MVS_E_HIP, "expand_accept launch failed"};
 }
 
 // ---------------------------------------------------------------------------
@@ -840,7 +862,7 @@ struct Engine {
         a.dist_thr = 0.05 / scale;
         a.thr = 0.7;
         a.exact_hits = ctx->d_exact.p;
-        if (mvs_launch_expand(&ctx->sc, recs(), &a, wid, s) != 0) throw Fail{MVS_E_HIP, "expand launch failed"};
+        expand_device(ctx, recs(), a, wid, s);
     }
 
     void fetch_sweep() { fetch_range(sweep_first, sweep_n); }
@@ -998,8 +1020,8 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
                    const double* R, const double* t, const double* Rp, mvs_ctx** out) {
     if (!out || !rgb || !K || !R || !t) return set_err(nullptr, Fail{MVS_E_ARG, "null argument"});
     *out = nullptr;
-    if (V < 1 || V > MVS_MAX_VIEWS || H < 16 || W < 16)
-        return set_err(nullptr, Fail{MVS_E_UNSUPPORTED, "need 1 <= V <= 256 and H, W >= 16"});
+    if (V < 1 || V > MVS_MAX_VIEWS || H < 16 || W < 16 || H > 65536 || W > 65536)
+        return set_err(nullptr, Fail{MVS_E_UNSUPPORTED, "need 1 <= V <= 256 and 16 <= H, W <= 65536"});
     std::unique_ptr<mvs_ctx> ctx(new mvs_ctx());
     ctx->device = device;
     int rc = guarded(ctx.get(), [&]() {
@@ -1017,8 +1039,19 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
         const int64_t stack_bytes = (int64_t)H * ctx->Wq * V * 4;
         ctx->d_stack.alloc(stack_bytes + 64);
         HIPCHK(hipMemsetAsync(ctx->d_stack.p, 0, stack_bytes + 64, ctx->stream));
-        if (mvs_launch_build_stack(ctx->d_rgb.p, ctx->d_stack.p, V, H, W, ctx->Wq, ctx->stream) != 0)
-            throw Fail{MVS_E_HIP, "build_stack launch failed"};
+        // view-major copy: 8 zero bytes left of column 0, >= 24 right of W-1,
+        // pitch a multiple of 16 (SceneDev)
+        ctx->sc.Wp = (W + 32 + 15) & ~15;
+        const int64_t gv_bytes = (int64_t)V * H * ctx->sc.Wp + 64;
+        ctx->d_gv.alloc(gv_bytes);
+        HIPCHK(hipMemsetAsync(ctx->d_gv.p, 0, gv_bytes, ctx->stream));
+        ctx->sc.V = V; ctx->sc.H = H; ctx->sc.W = W; ctx->sc.Wq = ctx->Wq;
+        ctx->sc.row_bytes = (int64_t)ctx->Wq * V * 4;
+        ctx->sc.stack = ctx->d_stack.p;
+        ctx->sc.rgb = ctx->d_rgb.p;
+        ctx->sc.gv = ctx->d_gv.p + 8;
+        if (mvs_launch_build_scene(&ctx->sc, ctx->d_rgb.p, ctx->d_stack.p, ctx->d_gv.p, ctx->stream) != 0)
+            throw Fail{MVS_E_HIP, "build_scene launch failed"};
         build_cameras(ctx.get(), K, R, t, Rp);
         ctx->K.assign(K, K + 9 * V);
         ctx->d_cams.alloc(V);
@@ -1026,20 +1059,7 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
         ctx->d_exact.alloc(1);
         HIPCHK(hipMemsetAsync(ctx->d_exact.p, 0, sizeof(int32_t), ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
-        ctx->sc.V = V; ctx->sc.H = H; ctx->sc.W = W; ctx->sc.Wq = ctx->Wq;
-        ctx->sc.row_bytes = (int64_t)ctx->Wq * V * 4;
-        ctx->sc.stack = ctx->d_stack.p;
-        ctx->sc.rgb = ctx->d_rgb.p;
         ctx->sc.cams = ctx->d_cams.p;
-        ctx->sc.Wp = ((W + 3) & ~3) + 16;
-        ctx->d_gv.alloc((size_t)V * H * ctx->sc.Wp + 64);
-        if (mvs_launch_build_gv(ctx->d_stack.p, ctx->d_gv.p, V, H, W, ctx->Wq, ctx->sc.Wp, ctx->stream) != 0)
-            throw Fail{MVS_E_HIP, "build_gv launch failed"};
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        ctx->sc.gv = ctx->d_gv.p;
-        for (int w = 0; w <= MVS_MAX_WID; ++w) ctx->sc.mom[w] = nullptr;
-        if (const char* vv = std::getenv("MVS_VARIANT")) ctx->variant = std::atoi(vv);
-        if (const char* cc = std::getenv("MVS_TILE_CHUNK")) ctx->chunk3 = std::max(32, std::min(512, std::atoi(cc)));
         if (const char* km = std::getenv("MVS_SCORE_KERNEL")) {
             if (!std::strcmp(km, "direct")) ctx->kernel_mode = 1;
             else if (!std::strcmp(km, "tiled")) ctx->kernel_mode = 2;
@@ -1057,9 +1077,11 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
 void mvs_ctx_destroy(mvs_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->scratch_ev) (void)hipEventSynchronize(ctx->scratch_ev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
+    if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
     delete ctx;
 }
 
@@ -1087,6 +1109,8 @@ int mvs_kernel_time(mvs_ctx* ctx, double* total_ms, int64_t* launches) {
         return 0;
     });
 }
+
+const char* mvs_timed_kernel(const mvs_ctx* ctx) { return ctx ? ctx->timed_name : ""; }
 
 int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp) {
     if (!ctx || !Rp) return MVS_E_ARG;
@@ -1368,7 +1392,7 @@ int mvs_expand_candidates(mvs_ctx* ctx, int64_t n_parents, const double* pc, con
         a.dist_thr = 0.05 / scale;
         a.thr = min_ncc;
         a.exact_hits = ctx->d_exact.p;
-        if (mvs_launch_expand(&ctx->sc, r, &a, wid, s) != 0) throw Fail{MVS_E_HIP, "expand launch failed"};
+        expand_device(ctx, r, a, wid, s);
         std::vector<uint8_t> col4(n_jobs * 4);
         HIPCHK(hipMemcpyAsync(X, c_.p + n_parents * 3, n_jobs * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(nX, n_.p + n_parents * 3, n_jobs * 3 * sizeof(double), hipMemcpyDeviceToHost, s));

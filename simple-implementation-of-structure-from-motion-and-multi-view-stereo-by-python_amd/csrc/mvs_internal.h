@@ -1,5 +1,6 @@
-// Internal declarations shared by the HIP kernels (mvs_kernels.hip) and the
-// host engine (mvs_engine.cpp).  Not part of the public C-ABI (include/mvs_amd.h).
+// Internal declarations shared by the HIP kernels (mvs_kernels.hip,
+// sfm_kernels.hip) and the host engine (mvs_engine.cpp).  Not part of the
+// public C-ABI (include/mvs_amd.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,19 +22,14 @@ struct CamDev {
     double pad[3];
 };
 
-// Window moments of one view at one pixel, 12 bytes: w = 1/sqrt(n S_bb - S_b^2)
-// (binary64, 0 for a constant window) and S_b.  S_bb is implied:
-// n S_bb - S_b^2 = rint(1/w^2) exactly (db < 2^31, w within 3 ulp).
-struct __attribute__((packed, aligned(4))) MomEntry {
-    double w;
-    uint32_t sb;
-};
-static_assert(sizeof(MomEntry) == 12, "12-byte moments entries");
-
-// Device-resident scene: the gray stack in quad-interleaved pixel-major
-// layout  stack[y][k][v][4] = gray_v(y, 4k..4k+3)  (k = quad index), so that
-// one window row of every view is one contiguous run, and one dword holds
-// four horizontally adjacent pixels of one view (v_dot4_u32_u8 operand).
+// Device-resident scene, two layouts of the same gray images (OpenCV's
+// BGR2GRAY fixed-point formula on the RGB data, HarrisFeatures.py:125):
+//  * stack[y][k][v][4] = gray_v(y, 4k..4k+3): one window row of every view is
+//    one contiguous run (the direct per-candidate scorers, lane = view);
+//  * gv[v][y][x], row pitch Wp (a multiple of 16) with 8 zero bytes left of
+//    column 0 and >= 24 right of column W-1: a tile region row of one view
+//    (columns x0-8 .. x0+23, x0 a multiple of 16) is two aligned 16-byte
+//    loads (the tiled matrix-core scorer).  gv points at column 0.
 struct SceneDev {
     int V, H, W;
     int Wq;            // quads per row, incl. one zero pad quad
@@ -41,15 +37,8 @@ struct SceneDev {
     const uint8_t* stack;
     const uint8_t* rgb;      // V*H*W*3 (colour lookups of expansion candidates)
     const CamDev* cams;
-    // view-major gray copy gv[v][y][x] (row pitch Wp = W + 16): the reference
-    // view's window rows are read with scalar (SMEM) loads
     const uint8_t* gv;
     int Wp;
-    // per-view window moments mom[wid][(y*W + x)*V + v] of the (2wid+1)^2
-    // window centred at (x, y) (zero where the window is invalid); built once
-    // per scene and wid -- the np.mean/np.std ingredients of ctNcc, which do
-    // not depend on the reference view
-    const struct MomEntry* mom[MVS_MAX_WID + 1];
 };
 
 // Inputs/outputs of one scoring batch (device pointers).
@@ -61,19 +50,20 @@ struct ScoreArgs {
     double* xy;           // n*2 (projection into ref view, MVS2.py:63)
     uint64_t* mask;       // n*words
     int32_t* count;       // n
-    double* avg;          // n
+    double* avg;          // n (may be null)
     int32_t* exact_hits;  // 1 counter: lanes that took the exact (numpy-order) path
 };
 
 // Scratch of the tiled scorer (device pointers, sized by the host).
-//   tile_count[ntiles+1], tile_off[ntiles+1], item_off[ntiles+1], n_items[1]
+//   tile_count[ntiles+2], tile_off[ntiles+1], item_off[ntiles+1]
 //   cand_key[n]  = tile (or -1 if the window is invalid), cand_rank[n],
-//   cand_pk[n]   = q | r << 11 | R << 22, sorted[n] = {id, pk} grouped by tile
-//   fix_list[n], fix_count[1]: candidates with a view decision inside the guard
-//   band, re-scored by k_score_fix (numpy-order ctNcc) after the tiled kernel
+//   cand_pk[n]   = (x - x0) | (y - y0) << 4 | R << 7 (pixel inside the tile),
+//   sorted[n]    = {id, pk} grouped by tile
+//   fix_list[n*groups], fix_count[1]: candidates with a view decision inside
+//   the guard band, re-scored by k_score_fix (numpy-order ctNcc) afterwards
 struct TiledArgs {
     int ntx, nty, ntiles;
-    int tw, th;                // tile size in pixels (x, y): 16x8 tiled kernels, 16x16 MFMA
+    int tw, th;                // tile size in pixels (x, y): 16 x 8
     int chunk;                 // candidates per work item
     int32_t* tile_count;
     int32_t* tile_off;
@@ -84,21 +74,20 @@ struct TiledArgs {
     int2* sorted;
     int32_t* fix_list;
     int32_t* fix_count;
-    // view groups (V > 64, k_score_tiledg): work item = (tile chunk, group of
-    // 64 views); per (candidate, group) partial count and sum of passing
-    // ncc*(n-1), reduced by k_group_finalize.  groups = 1 otherwise.
+    // view groups (V > 64): work unit = (work item, group of 64 views); per
+    // (candidate, group) partial count and sum of passing ncc, reduced by
+    // k_group_finalize.  groups = 1 otherwise.
     int groups;
     int32_t* part_cnt;         // n*groups
     double* part_sum;          // n*groups
-    int32_t* xq;               // 8 work-queue heads, one per XCD label (blockIdx % 8)
     // k_tile_scan leaves every counter zero for the next batch (it zeroes the
-    // bin counts after reading them and the queue heads / fix_count before the
+    // bin counts after reading them and the queue head / fix_count before the
     // scorer uses them); zero_first = 1 asks the launcher to clear them first
     // (new scratch, or a previous sequence that did not complete)
     int zero_first;
-    // work items in the order the scorers take them (k_tile_scan): every full
+    // work items in the order the scorer takes them (k_tile_scan): every full
     // chunk first, then the partial (last) chunks by decreasing size, so the
-    // dynamic queues end on the shortest items; int2 = (tile, chunk index)
+    // dynamic queue ends on the shortest items; int2 = (tile, chunk index)
     int2* items;
 };
 
@@ -133,25 +122,62 @@ struct ExpandArgs {
     int32_t* exact_hits;
 };
 
+// Geometry of the tiled scorer (host side sizes scratch with it).
+#define MVS_TILE_W 16
+#define MVS_TILE_H 8
+#define MVS_MMA_CHUNK 1024    // candidates per work item, V <= 64 (whole tiles, as a rule)
+#define MVS_GROUP_VIEWS 64    // views per group when V > 64
+#define MVS_GROUP_CHUNK 64    // candidates per work item when V > 64
+
 extern "C" {
-int mvs_launch_build_stack(const uint8_t* d_rgb, uint8_t* d_stack, int V, int H, int W, int Wq,
+// RGB -> stack and gv (one pass, coalesced on both sides); the caller zeroes
+// both buffers first (pads)
+int mvs_launch_build_scene(const SceneDev* sc, const uint8_t* d_rgb, uint8_t* d_stack, uint8_t* d_gv_base,
                            hipStream_t s);
-// ev0/ev1 (may be null): recorded on s immediately before and after the
-// dominant scoring kernel (k_score / k_score_tiled3) -- kernel timing for bench.py
+// direct per-candidate scorer (k_score); ev0/ev1 (may be null) are recorded
+// on s immediately before and after the kernel
 int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s,
                      hipEvent_t ev0, hipEvent_t ev1);
-int mvs_launch_build_gv(const uint8_t* d_stack, uint8_t* d_gv, int V, int H, int W, int Wq, int Wp,
-                        hipStream_t s);
-int mvs_launch_build_moments(const SceneDev* sc, int wid, MomEntry* d_mom, hipStream_t s);
-// Tile geometry of the tiled scorers for a W x H image (so the host can size
-// scratch): mfma != 0 -> the MFMA scorer's 16x16 tiles, else 16x8.
-void mvs_tiled_geometry(int W, int H, int mfma, int* tw, int* th, int* ntx, int* nty);
+// tiled scorer: k_bin, k_tile_scan, k_scatter, k_score_mma (timed by ev0/ev1),
+// [k_group_finalize,] k_score_fix
 int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
-                           int variant, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+                           hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+// dynamic LDS bytes of k_score_mma (0 if the configuration is unsupported)
+size_t mvs_mma_lds_bytes(int V, int wid);
+// name of the kernel mvs_launch_score / mvs_launch_score_tiled time for (V, wid)
+const char* mvs_timed_kernel_name(int V, int wid, int tiled);
+// patch_expansion children, one wave each: geometry + direct photo test +
+// accept test (small sweeps)
 int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, int wid,
                       hipStream_t s);
-// SfM front-end (HarrisFeatures.py): Harris response + dilate + global max +
-// per-row counts and offsets (rowoff[H] = total), then the [col, row] write
+// the same split for large sweeps: geometry (+ colour, projection, cell) of
+// every child, then the children's photo test through the tiled scorer, then
+// the accept test from the scored counts
+int mvs_launch_expand_geom(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, hipStream_t s);
+int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hipStream_t s);
+// Packed record rows for the multi-GPU stage exchange: int64 words
+// [c0 c1 c2 n0 n1 n2 x y | mask[words] | R + count<<32 | cell0 + cell1<<32 | rgba + accept<<32]
+int mvs_launch_pack_records(RecordsDev rec, int words, int64_t first, int64_t n, int64_t* out,
+                            hipStream_t s);
+int mvs_launch_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n,
+                              const int64_t* in, hipStream_t s);
+int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
+                           int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
+// stage output order on the device (reconstruct_from_Q, MVS2.py:159-173):
+// key[e] = (min view of record events[e]) * nci*ncj + cell x * ncj + cell y,
+// or ~0 for an event that is never emitted
+int mvs_launch_event_keys(RecordsDev rec, int words, const int32_t* events, int64_t n_events,
+                          int nci, int ncj, uint64_t* keys, hipStream_t s);
+// rows[i] = [c, rgb] of record idx[i] as float64 (the PLY rows)
+int mvs_launch_gather_rows(RecordsDev rec, const int32_t* idx, int64_t n, double* rows, hipStream_t s);
+// stable device sort of (key, value) pairs over the low `bits` key bits;
+// tmp == NULL sizes the scratch (*tmp_bytes)
+int mvs_sort_pairs(void* tmp, size_t* tmp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                   const int32_t* vals_in, int32_t* vals_out, int64_t n, int bits, hipStream_t s);
+
+// SfM front-end (HarrisFeatures.py, sfm_kernels.hip): Harris response +
+// dilate + global max + per-row counts and offsets (rowoff[H] = total), then
+// the [col, row] write
 int mvs_launch_harris(const SceneDev* sc, int v, double k, float* resp, float* dil, uint32_t* maxkey,
                       int32_t* rowcnt, int32_t* rowoff, hipStream_t s);
 int mvs_launch_harris_write(const SceneDev* sc, const float* dil, const uint32_t* maxkey,
@@ -161,12 +187,4 @@ int mvs_launch_gather_desc(const SceneDev* sc, int v, const int32_t* rc, int64_t
 int mvs_launch_match_rows(const uint32_t* dA, const int32_t* SA, const int32_t* SSA, int64_t nA,
                           const uint32_t* dB, const int32_t* SB, const int32_t* SSB, int64_t nB,
                           int npx, double thr, int32_t* best, hipStream_t s);
-// Packed record rows for the multi-GPU stage exchange: int64 words
-// [c0 c1 c2 n0 n1 n2 x y | mask[words] | R + count<<32 | cell0 + cell1<<32 | rgba + accept<<32]
-int mvs_launch_pack_records(RecordsDev rec, int words, int64_t first, int64_t n, int64_t* out,
-                            hipStream_t s);
-int mvs_launch_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n,
-                              const int64_t* in, hipStream_t s);
-int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
-                           int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
 }

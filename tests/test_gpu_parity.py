@@ -23,16 +23,14 @@ def ctx(pkg, dino):
     c.close()
 
 
-@pytest.fixture(scope="module", params=["direct", "tiled", "tiled3", "tiled4", "tiled5"])
+@pytest.fixture(scope="module", params=["direct", "tiled"])
 def kctx(request, pkg, dino):
-    """A context forced onto one scoring kernel (MVS_SCORE_KERNEL; "tiled3" /
-    "tiled4" / "tiled5" = the tiled path with MVS_VARIANT 10 / 11 / 15:
-    k_score_tiled3, the experimental k_score_tiled4, k_score_tiled5 — the
-    default "tiled" path is k_score_tiled5 too)."""
+    """A context forced onto one scoring path (MVS_SCORE_KERNEL): the direct
+    per-candidate k_score, or the tiled matrix-core k_score_mma for every
+    batch size."""
     import os
     rgb, K, R, t = dino
-    variant = {"tiled3": "10", "tiled4": "11", "tiled5": "15"}.get(request.param)
-    env = {"MVS_SCORE_KERNEL": "tiled" if variant else request.param, "MVS_VARIANT": variant}
+    env = {"MVS_SCORE_KERNEL": request.param}
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
         if v is None:
@@ -284,7 +282,8 @@ def _smooth_ring(pkg, V, H=96, W=128):
 
 @pytest.mark.parametrize("V,wid", [(68, 5), (100, 3), (256, 3), (100, 1), (132, 2), (200, 4)])
 def test_view_groups_wid_and_partial_group(pkg, orc, V, wid):
-    """k_score_tiledg with a 4-view last group (V = 68) and at wid 3."""
+    """The view-group path of k_score_mma (V > 64) with a 4-view last group
+    (V = 68), every window size."""
     H, W = 96, 128
     rgb, K, R, t = _smooth_ring(pkg, V, H, W)
     with pkg.MvsContext(rgb, K, R, t) as cx:
@@ -329,9 +328,9 @@ def test_view_groups_threshold_on_reference_value(pkg, orc):
 
 @pytest.mark.parametrize("V", [5, 32, 64, 100, 102, 192, 256])
 def test_view_count_variants(pkg, orc, V):
-    """Lane-slot layouts: V < 64, one extra slot, and the 4-slot 256-view case;
-    3000 candidates take the tiled scorers (k_score_tiled3, or the view-group
-    k_score_tiledg for V > 64 with V % 4 == 0; V = 102 stays on k_score)."""
+    """View counts on both paths: 3000 candidates take k_score_mma (16-view
+    blocks, V % 16 != 0 padded; view groups for V > 64), the direct path's
+    lane slots are covered by the kctx tests."""
     syn = pkg.synthetic
     H, W = 96, 128
     rgb, K, R, t = syn.ring_scene(V=V, H=H, W=W, seed=V)

@@ -1,0 +1,204 @@
+"""Entry points and configurations beyond the core parity tests (HIP path
+against the oracle / the reference's golden vectors):
+
+* MyPatch.photo_consistenecy_test, the per-candidate drop-in (MVS2.py:62-77),
+  on the reference's own 300 photo-test cases;
+* mvs_expand_candidates (MVS2.py:329-369) against the oracle, on the direct
+  (< 2048 jobs) and the tiled (>= 2048) path;
+* 47 views at 640x480 (BASELINE config 3's view count, V % 16 != 0) at the
+  bench's candidate distribution and through a 2,000-pop stage;
+* images wider than 2048 pixels;
+* device calls on a caller's stream followed by host calls on the context's
+  stream (the context's scratch is ordered across streams).
+"""
+import numpy as np
+import pytest
+
+from conftest import bench_candidates
+
+pytestmark = pytest.mark.gpu
+
+AVG_TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg, dino):
+    import torch
+    assert torch.cuda.is_available(), "GPU test without a GPU"
+    rgb, K, R, t = dino
+    c = pkg.MvsContext(rgb, K, R, t, device=0)
+    yield c
+    c.close()
+
+
+def test_mypatch_dropin_golden(pkg, dino, func_golden):
+    """The reference's per-candidate call (MyPatch.photo_consistenecy_test,
+    MVS2.py:62-77): V list (views in increasing order, each with the
+    projection into the reference view) and avg_ncc_score, on the 300 photo
+    tests recorded from the reference itself."""
+    import importlib
+    mvs2 = importlib.import_module(pkg.__name__ + ".MVS2")
+    rgb, K, R, t = dino
+    imgs = [rgb[v] for v in range(len(rgb))]
+    par_K = {v: K[v] for v in range(len(K))}
+    par_r = {v: R[v] for v in range(len(R))}
+    par_t = {v: t[v].reshape(3, 1) for v in range(len(t))}
+    f = func_golden
+    for k in range(len(f["pt_R"])):
+        p = mvs2.MyPatch(f["pt_c"][k], None, int(f["pt_R"][k]), [], None, None)
+        V = p.photo_consistenecy_test(imgs, par_K, par_r, par_t, float(f["pt_thr"][k]))
+        m = int(f["pt_mask"][k, 0])
+        views = [b for b in range(64) if (m >> b) & 1]
+        assert [e[0] for e in V] == views, k
+        assert len(V) == int(f["pt_count"][k])
+        for e in V:
+            assert e[1] == f["pt_xy"][k, 0] and e[2] == f["pt_xy"][k, 1]
+        assert abs(p.avg_ncc_score - f["pt_avg"][k]) <= AVG_TOL
+    mvs2.clear_context_cache()
+
+
+def test_mypatch_context_follows_image_edits(pkg, dino):
+    """The cached scene context sees in-place edits of the images (sampled
+    content fingerprint) and replaced arrays."""
+    import importlib
+    mvs2 = importlib.import_module(pkg.__name__ + ".MVS2")
+    rgb, K, R, t = dino
+    imgs = [rgb[v].copy() for v in range(len(rgb))]
+    par = ({v: K[v] for v in range(48)}, {v: R[v] for v in range(48)},
+           {v: t[v].reshape(3, 1) for v in range(48)})
+    c1 = mvs2.scene_context(imgs, *par)
+    assert mvs2.scene_context(imgs, *par) is c1
+    imgs[3][0, :, :] = 7                       # row 0 is sampled
+    c2 = mvs2.scene_context(imgs, *par)
+    assert c2 is not c1
+    imgs[5] = imgs[5].copy()                    # a new array object
+    assert mvs2.scene_context(imgs, *par) is not c2
+    mvs2.clear_context_cache()
+
+
+def _parents(K, R, t, n, seed):
+    """Parent patches on the object's depth range: centre, normal toward the
+    reference camera, projection into the reference view (MVS2.py:238-247)."""
+    from oracle import oracle as orc
+    c, ref = bench_candidates(n, K, R, t, seed=seed)
+    pn = np.empty_like(c)
+    pxy = np.empty((n, 2))
+    for k in range(n):
+        O = -(R[ref[k]].T @ t[ref[k]].ravel())
+        d = O - c[k]
+        pn[k] = d / np.linalg.norm(d)
+        pxy[k] = orc.project(K[ref[k]], orc.rodrigues_roundtrip(R[ref[k]]), t[ref[k]].ravel(), c[k])
+    return c, pn, pxy, ref
+
+
+@pytest.mark.parametrize("n_jobs", [700, 4096])
+def test_expand_candidates_vs_oracle(ctx, oracle_scene, dino, n_jobs):
+    """mvs_expand_candidates: every output of every job bit-exact against the
+    oracle's restatement of MVS2.py:329-369 (direct path below 2,048 jobs,
+    geometry + tiled photo test + accept above)."""
+    rgb, K, R, t = dino
+    rng = np.random.default_rng(n_jobs)
+    pc, pn, pxy, _ = _parents(K, R, t, 400, seed=n_jobs)
+    jp = rng.integers(0, len(pc), n_jobs).astype(np.int32)
+    jv = rng.integers(0, 48, n_jobs).astype(np.int32)
+    jd = rng.choice(np.array([-1, 1], np.int32), n_jobs)
+    got = ctx.expand_candidates(pc, pn, pxy, jp, jv, jd, cell_size=2, scale=10.0, wid=5, min_ncc=0.7)
+    exp = oracle_scene.expand_candidates(pc, pn, pxy, jp, jv, jd, cell_size=2, scale=10.0, wid=5, thr=0.7)
+    for name, g, e in zip(("X", "nX", "color", "xy", "mask", "count", "accept"), got, exp):
+        assert np.array_equal(g, e), name
+    assert exp[5].sum() > 0
+
+
+@pytest.fixture(scope="module")
+def dino47(dino):
+    rgb, K, R, t = dino
+    return rgb[:47].copy(), K[:47].copy(), R[:47].copy(), t[:47].copy()
+
+
+def test_view_count_47_bench_distribution(pkg, orc, dino47):
+    """47 views of 640x480 (BASELINE config 3's view count; the last 16-view
+    block of the matrix-core scorer is padded): 2^18 candidates of the bench's
+    distribution bit-exact against the oracle."""
+    import os
+    rgb, K, R, t = dino47
+    c, ref = pkg.synthetic.candidates(1 << 18, K, R, t, seed=47)
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        got = cx.score(c, ref, 0.7, 5)
+    exp = orc.Scene(rgb, K, R, t).score_batch(c, ref, 0.7, 5, nthreads=min(os.cpu_count() or 1, 16))
+    for g, e in zip(got[:3], exp[:3]):
+        assert np.array_equal(g, e)
+    np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+    assert got[2].sum() > 0
+
+
+def test_view_count_47_stage(pkg, orc, dino47, seeds):
+    """The 47-view scene through a 2,000-pop stage (seeds restricted to
+    tracks inside views 0-46), bit-exact against the oracle stage."""
+    rgb, K, R, t = dino47
+    off, ov, oxy = seeds["track_off"], seeds["obs_view"], seeds["obs_xy"]
+    keep_off, keep_v, keep_xy = [0], [], []
+    for k in range(len(off) - 1):
+        v = ov[off[k]:off[k + 1]]
+        if (v < 47).all():
+            keep_v += list(v)
+            keep_xy += list(oxy[off[k]:off[k + 1]])
+            keep_off.append(len(keep_v))
+    args = (np.array(keep_off, np.int64), np.array(keep_v, np.int32), np.array(keep_xy, np.float32))
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        ini, allp, st = cx.stage(*args, cell_size=2, scale=10.0, wid=5, max_pops=2000)
+    oini, oall, ost = orc.Scene(rgb, K, R, t).mvs_stage(*args, scale=10.0, max_pops=2000)
+    assert st["pops"] == ost["pops"] and st["tests"] == ost["tests"]
+    assert np.array_equal(ini, oini) and np.array_equal(allp, oall)
+    assert len(allp) > 1000
+
+
+def test_wide_image(pkg, orc):
+    """W = 2100 (> 2048): tile coordinates are stored relative to the tile,
+    so any width/height works; every output against the oracle."""
+    H, W, V = 64, 2100, 6
+    rgb, K, R, t = pkg.synthetic.ring_scene(V=V, H=H, W=W, seed=3)
+    rgb = ((rgb.astype(np.uint16) + np.roll(rgb, 1, axis=0)) // 2).astype(np.uint8)
+    c, ref = pkg.synthetic.candidates(6000, K, R, t, W=W, H=H, seed=3)
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        got = cx.score(c, ref, 0.2, 5)
+    exp = orc.Scene(rgb, K, R, t).score_batch(c, ref, 0.2, 5)
+    for g, e in zip(got[:3], exp[:3]):
+        assert np.array_equal(g, e)
+    assert (got[2] > 0).any() and (np.asarray(got[0])[:, 0] > 2048).any()
+
+
+def test_device_call_on_other_stream_then_host_call(ctx, oracle_scene, dino):
+    """A scoring call on a caller's stream, then at once a host-pointer call on
+    the context's own stream: the second waits for the first's use of the
+    shared scratch, both results are right."""
+    import torch
+    rgb, K, R, t = dino
+    c1, r1 = bench_candidates(1 << 16, K, R, t, seed=31)
+    c2, r2 = bench_candidates(5000, K, R, t, seed=32)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        tc = torch.from_numpy(c1).to(dev)
+        tr = torch.from_numpy(r1).to(dev)
+        xy = torch.empty((len(r1), 2), dtype=torch.float64, device=dev)
+        mask = torch.empty((len(r1), 1), dtype=torch.int64, device=dev)
+        count = torch.empty(len(r1), dtype=torch.int32, device=dev)
+        avg = torch.empty(len(r1), dtype=torch.float64, device=dev)
+    ctx.score_device(tc, tr, xy, mask, count, avg, 0.7, 5, stream=s.cuda_stream)
+    got2 = ctx.score(c2, r2, 0.7, 5)                     # context stream, right away
+    s.synchronize()
+    exp1 = oracle_scene.score_batch(c1, r1, 0.7, 5, nthreads=8)
+    exp2 = oracle_scene.score_batch(c2, r2, 0.7, 5, nthreads=8)
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), exp1[1])
+    assert np.array_equal(count.cpu().numpy(), exp1[2])
+    assert np.array_equal(got2[1], exp2[1]) and np.array_equal(got2[2], exp2[2])
+
+
+def test_timed_kernel_name(ctx, dino):
+    rgb, K, R, t = dino
+    c, ref = bench_candidates(4096, K, R, t, seed=1)
+    ctx.kernel_timing(True)
+    ctx.score(c, ref, 0.7, 5)
+    ms, k = ctx.kernel_time()
+    ctx.kernel_timing(False)
+    assert k == 1 and ms > 0 and ctx.timed_kernel() == "k_score_mma"
