@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=500000,
                     help="candidates the single-threaded oracle scores (~10 s)")
     ap.add_argument("--secondary-wid", type=int, default=3)
+    ap.add_argument("--no-stage", action="store_true", help="skip the full-stage secondary")
     ap.add_argument("--kernel", choices=["auto", "direct", "tiled"], default="auto",
                     help="scoring kernel (MVS_SCORE_KERNEL)")
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",

@@ -30,6 +30,9 @@ def build(force=False, verbose=False, stamps=False):
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           # no wave-aggregated global atomics: their immediate wait on the
+           # return value would also drain the scorer's LDS-DMA prefetch
+           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
     if stamps:
         cmd.append("-DMVS_STAMPS")

@@ -306,7 +306,7 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand, t_pcnt;
-    DevBuf<int2> t_items;
+    DevBuf<int4> t_items;
     DevBuf<double> t_psum;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
     DevBuf<float> f_resp, f_dil;

@@ -26,10 +26,11 @@ struct CamDev {
 // BGR2GRAY fixed-point formula on the RGB data, HarrisFeatures.py:125):
 //  * stack[y][k][v][4] = gray_v(y, 4k..4k+3): one window row of every view is
 //    one contiguous run (the direct per-candidate scorers, lane = view);
-//  * gv[v][y][x], row pitch Wp (a multiple of 16) with 8 zero bytes left of
-//    column 0 and >= 24 right of column W-1: a tile region row of one view
-//    (columns x0-8 .. x0+23, x0 a multiple of 16) is two aligned 16-byte
-//    loads (the tiled matrix-core scorer).  gv points at column 0.
+//  * gv[v][y][x] = g - 128 as a signed byte (the i8 operands of the tiled
+//    matrix-core scorer), row pitch Wp (a multiple of 16) with 8 pad bytes
+//    left of column 0 and >= 24 right of column W-1: a tile region row of
+//    one view (columns x0-8 .. x0+23, x0 a multiple of 16) is two aligned
+//    16-byte pieces.  gv points at column 0.
 struct SceneDev {
     int V, H, W;
     int Wq;            // quads per row, incl. one zero pad quad
@@ -87,8 +88,9 @@ struct TiledArgs {
     int zero_first;
     // work items in the order the scorer takes them (k_tile_scan): every full
     // chunk first, then the partial (last) chunks by decreasing size, so the
-    // dynamic queue ends on the shortest items; int2 = (tile, chunk index)
-    int2* items;
+    // dynamic queue ends on the shortest items; int4 = (tile, first sorted
+    // candidate, candidates, 0)
+    int4* items;
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).

@@ -16,6 +16,7 @@
 // -ffp-contract=off (products that numpy/OpenBLAS fuse are written as fma()).
 #include <algorithm>
 #include <cstdlib>
+#include <utility>
 
 #include <hipcub/hipcub.hpp>
 
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(256) void k_build_scene(const SceneDev sc, const ui
                     }
                 }
                 squad[qd][vv] = word;
-                *(uint32_t*)(gv + ((int64_t)(v0 + vv) * sc.H + y) * sc.Wp + x0 + 4 * qd) = word;
+                // gv: signed bytes s = g - 128 (the tiled scorer's operands)
+                *(uint32_t*)(gv + ((int64_t)(v0 + vv) * sc.H + y) * sc.Wp + x0 + 4 * qd) = word ^ 0x80808080u;
             }
         }
         __syncthreads();
@@ -469,9 +471,9 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
         rc += c;
         ri += (c + t.chunk - 1) / t.chunk;
         const int full = c / t.chunk, rem = c - full * t.chunk;
-        for (int j = 0; j < full; ++j) t.items[rf + j] = make_int2(k, j);
+        for (int j = 0; j < full; ++j) t.items[rf + j] = make_int4(k, rc - c + j * t.chunk, t.chunk, 0);
         rf += full;
-        if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int2(k, full);
+        if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int4(k, rc - c + full * t.chunk, rem, 0);
         t.tile_count[k] = 0;          // clean for the next batch's k_bin
     }
     if (tid == 1023) {
@@ -538,26 +540,26 @@ struct MmaGeom {
 };
 
 // per-wave slot of one candidate of the M-block being scored
-struct alignas(16) CandInfo {
+struct alignas(16) CandInfoG {
     int32_t px, R, Sa, da;   // pixel in the tile, reference view, its window moments
     double ca;               // n / ((n-1) sqrt(da))
     float tkda;              // (thr (n-1)/n)^2 da
     int32_t idx;
 };
 
-struct MmaLds {
+struct MmaLdsG {
     int reg, mom, ci, wsum, zero, areg, asum, total;
 };
 
 template <int WID>
-__host__ __device__ inline MmaLds mma_lds(int VR, int VP, bool grouped) {
+__host__ __device__ inline MmaLdsG mma_lds_g(int VR, int VP, bool grouped) {
     using G = MmaGeom<WID>;
-    MmaLds L;
+    MmaLdsG L;
     L.reg = 0;
     L.mom = VR * G::VS;
     const int htmp = G::ROWS * 16 * VP * 4, mom = 128 * VP * 8;   // aliased: horizontal sums, then the table
     L.ci = L.mom + (htmp > mom ? htmp : mom);
-    L.wsum = L.ci + kMmaWaves * 16 * (int)sizeof(CandInfo);
+    L.wsum = L.ci + kMmaWaves * 16 * (int)sizeof(CandInfoG);
     L.zero = L.wsum + kMmaWaves * 16 * 8;
     L.areg = L.zero + 32;
     L.asum = L.areg + (grouped ? kGroupChunk * G::NB * 32 : 0);
@@ -568,14 +570,8 @@ __host__ __device__ inline MmaLds mma_lds(int VR, int VP, bool grouped) {
 // 4-bit column mask -> byte mask
 DEV uint32_t byte_mask(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xffu; }
 
-DEV uint4 load_signed(const uint8_t* p) {
-    uint4 w = *(const uint4*)p;
-    w.x ^= 0x80808080u;
-    w.y ^= 0x80808080u;
-    w.z ^= 0x80808080u;
-    w.w ^= 0x80808080u;
-    return w;
-}
+// gv holds s = g - 128 already
+DEV uint4 load_signed(const uint8_t* p) { return *(const uint4*)p; }
 
 // 1/k for k = 0..64 (entry 0 unused), correctly rounded at compile time
 struct RecipTable {
@@ -587,7 +583,7 @@ struct RecipTable {
 __constant__ constexpr RecipTable c_recip{};
 
 template <int WID, int NBLK, bool GROUPED>
-__global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, const ScoreArgs a,
+__global__ __launch_bounds__(kMmaThreads) void k_score_mma_g(const SceneDev sc, const ScoreArgs a,
                                                            const TiledArgs t) {
     using G = MmaGeom<WID>;
     constexpr int NB = G::NB, NPX = G::NPX, ROWS = G::ROWS, KS = G::KS, VS = G::VS, C0 = G::C0;
@@ -599,11 +595,11 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     const int V = sc.V;
     const int NG = GROUPED ? t.groups : 1;
     const int words = (V + 63) >> 6;
-    const MmaLds L = mma_lds<WID>(GROUPED ? kGroupViews : V, VP, GROUPED);
+    const MmaLdsG L = mma_lds_g<WID>(GROUPED ? kGroupViews : V, VP, GROUPED);
     uint8_t* reg = smem + L.reg;
     uint32_t* htmp = (uint32_t*)(smem + L.mom);
     int2* mom = (int2*)(smem + L.mom);
-    CandInfo* ci = (CandInfo*)(smem + L.ci) + wave * 16;
+    CandInfoG* ci = (CandInfoG*)(smem + L.ci) + wave * 16;
     double* wsum = (double*)(smem + L.wsum) + wave * 16;
     uint8_t* areg = smem + L.areg;
     int2* asum = (int2*)(smem + L.asum);
@@ -623,11 +619,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
         if (unit >= n_units) break;
         const int item = GROUPED ? unit / NG : unit;
         const int g = GROUPED ? unit - item * NG : 0;
-        const int2 itv = t.items[item];
+        const int4 itv = t.items[item];
         const int tile = __builtin_amdgcn_readfirstlane(itv.x);
-        const int cb = __builtin_amdgcn_readfirstlane(t.tile_off[tile] + itv.y * t.chunk);
-        const int ce = min(cb + t.chunk, __builtin_amdgcn_readfirstlane(t.tile_off[tile + 1]));
-        const int nc = ce - cb;
+        const int cb = __builtin_amdgcn_readfirstlane(itv.y);
+        const int nc = __builtin_amdgcn_readfirstlane(itv.z);
         const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
         const int x0 = tx * MVS_TILE_W, yr0 = ty * MVS_TILE_H - WID;
         const int vb = g * kGroupViews;
@@ -782,7 +777,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             }
             // per-candidate constants, shared with the wave's other lanes
             if (kh == 0) {
-                CandInfo c;
+                CandInfoG c;
                 c.px = rrel * 16 + qrel;
                 int Sa = 0, da = 0;
                 if (valid) {
@@ -811,7 +806,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             double sacc[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const CandInfo c = ci[4 * kh + i];
+                const CandInfoG c = ci[4 * kh + i];
                 double sa = 0.0;
                 Gd[i] = 0;
 #pragma unroll
@@ -880,6 +875,508 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             }
         }
         __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_score_mma (V <= 64).  A workgroup (16 waves) takes one work item (the
+// candidates of one 16x8 pixel tile, at most kMmaChunk) from a dynamic queue:
+//   1. the item's window region of every view (signed bytes s = g - 128,
+//      [view][ROWS rows][32 columns], two aligned 16-B loads of gv per view
+//      row) and its candidate list go to LDS; the NEXT item's region is
+//      loaded into registers meanwhile (issued after this item is staged,
+//      written to LDS at the top of the next iteration), so the global
+//      latency hides behind phases 2-3;
+//   2. per (pixel, view) of the tile: S_b and w = 1/sqrt(n S_bb - S_b^2) in
+//      binary64 (NaN for a constant window: ctNcc's nan, never passes), from
+//      horizontal v_dot4_i32_i8 prefix sums and vertical sums;
+//   3. 16 candidates per wave and M-block: C[m][v] = sum over the window of
+//      s_R s_v by v_mfma_i32_16x16x64_i8 (A = the reference window masked to
+//      candidate m's window, B = view v's region), exact;
+//   4. per (candidate, view): num = n C - S_a S_b (the n S_ab - S_a S_b of
+//      ctNcc, shift invariant), ncc = n/(n-1) num w_a w_b, so
+//      ncc > thr  <=>  num w_b > T = thr (n-1)/(n w_a): one binary32 fma,
+//      with a relative guard band of 2e-6 |T| (the binary32 roundings add
+//      < 3e-7 |T|); a candidate with any pair in the band is re-scored by
+//      k_score_fix (numpy-order ctNcc).  avg_ncc_score = n/(n-1) w_a
+//      sum(num w_b) / cnt in binary64.
+// ---------------------------------------------------------------------------
+#ifdef MVS_STAMPS
+// diagnostic build only: per-workgroup cycle sums of the scorer's phases
+// (slot 0 items, 1 staging + barrier, 2 moments, 3 candidates, 4 wave 0's own
+// candidate time, 5 wave 0's M-blocks), read by mvs_read_stamps
+__device__ unsigned long long g_stamps[4096 * 8];
+#define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(slot, val) \
+    do { if (threadIdx.x == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 8 + (slot)], (unsigned long long)(val)); } while (0)
+#define STAMP_ADD_W0(slot, val) \
+    do { if ((threadIdx.x & 1023) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 8 + (slot)], (unsigned long long)(val)); } while (0)
+#else
+#define STAMP(var)
+#define STAMP_ADD(slot, val)
+#define STAMP_ADD_W0(slot, val)
+#endif
+
+struct alignas(16) CandInfo {
+    int32_t px, R, Sa, idx;   // pixel in the tile, reference view (-1: no candidate), -S_a, batch index
+    float T, gT;              // decision threshold on num w_b and its guard band
+    double ca;                // n / (n-1) * w_a
+};
+
+// per-wave slot: ballots (pass per (i, nb), guard per i) and the candidates' sums
+template <int NBLK>
+struct WaveSlot {
+    uint32_t pm[2 * 4 * NBLK];
+    uint32_t gd[8];
+    double wsum[16];
+};
+
+// LDS layout: region | S_b table, w table (binary64), [w table (binary32)]
+// (the tables alias the horizontal sums of phase 2) | per-wave candidate
+// slots | per-wave ballots and sums | the item's candidates | 32 zero bytes
+struct MmaLds {
+    int reg, regsz, sb, w, wf, ci, wp, cand, zero, total;
+};
+
+// Dynamic LDS of k_score_mma.  DB: the two region buffers and the two
+// candidate buffers are static LDS arrays of the kernel (the next item's
+// region and candidates land by LDS-DMA during this item's candidates), so
+// the dynamic part holds only the tables and slots; otherwise one region and
+// one candidate buffer come first.  WF: a binary32 copy of the w table.
+template <int WID, int NBLK, bool WF, bool DB>
+__host__ __device__ constexpr MmaLds mma_lds(int V) {
+    using G = MmaGeom<WID>;
+    constexpr int VP = 16 * NBLK;
+    MmaLds L{};
+    L.reg = 0;
+    L.regsz = V * G::VS;                               // VS is a multiple of 32
+    L.sb = DB ? 0 : L.regsz;
+    L.w = L.sb + 128 * VP * 4;
+    L.wf = L.w + 128 * VP * 8;
+    const int htmp = G::ROWS * 16 * VP * 4, tab = 128 * VP * (WF ? 16 : 12);
+    L.ci = L.sb + (htmp > tab ? htmp : tab);
+    L.wp = L.ci + kMmaWaves * 16 * (int)sizeof(CandInfo);
+    L.cand = L.wp + kMmaWaves * (int)sizeof(WaveSlot<NBLK>);
+    L.zero = L.cand + (DB ? 0 : kMmaChunk * 8);
+    L.total = L.zero + 32;
+    return L;
+}
+
+// static LDS of k_score_mma: region and candidate buffers (DB) + small slots
+template <int WID, int NBLK, bool DB>
+__host__ __device__ constexpr int mma_static_lds() {
+    return (DB ? 2 * (16 * NBLK * MmaGeom<WID>::VS + kMmaChunk * 8) : 64) + 8 + 4 + 65 * 8 + 64;
+}
+
+// what fits in 160 KiB beside the rest at this NBLK (1 workgroup of 16 waves
+// per CU): double buffering first, then the binary32 w copy
+template <int WID, int NBLK>
+__host__ __device__ constexpr bool mma_db() {
+    return mma_lds<WID, NBLK, false, true>(16 * NBLK).total + mma_static_lds<WID, NBLK, true>() <= 160 * 1024;
+}
+template <int WID, int NBLK>
+__host__ __device__ constexpr bool mma_wf() {
+    return mma_lds<WID, NBLK, true, mma_db<WID, NBLK>()>(16 * NBLK).total +
+               mma_static_lds<WID, NBLK, mma_db<WID, NBLK>()>() <= 160 * 1024;
+}
+template <int WID, int NBLK>
+__host__ __device__ constexpr MmaLds mma_layout(int V) {
+    return mma_lds<WID, NBLK, mma_wf<WID, NBLK>(), mma_db<WID, NBLK>()>(V);
+}
+
+// v_writelane_b32 (lane LANE of v takes the wave-uniform x) through the LLVM
+// intrinsic, so that the hazard recognizer sees it: a VALU write of the
+// source SGPR (a ballot's v_cmp) needs wait states before v_writelane reads
+// it, which inline asm would hide from the compiler
+extern "C" __device__ int mvs_llvm_writelane(int x, int lane, int v) __asm("llvm.amdgcn.writelane.i32");
+template <int LANE>
+DEV uint32_t writelane(uint32_t v, uint32_t x) {
+    return (uint32_t)mvs_llvm_writelane((int)x, LANE, (int)v);
+}
+
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N-1>)
+template <class F, int... I>
+DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+DEV void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int WID, int NBLK, bool FAST>
+__global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
+                                                           const int4* __restrict__ items,
+                                                           const int2* __restrict__ sorted) {
+    using G = MmaGeom<WID>;
+    constexpr int NB = G::NB, NPX = G::NPX, ROWS = G::ROWS, KS = G::KS, VS = G::VS, C0 = G::C0;
+    constexpr int VP = 16 * NBLK;                         // views per table row
+    constexpr bool WF = mma_wf<WID, NBLK>(), DB = mma_db<WID, NBLK>();
+    constexpr int RPV = VS / 32;                          // region rows per view incl. the pad row
+    constexpr int PF = (VP * RPV * 2 + kMmaThreads - 1) / kMmaThreads;   // 16-B pieces per thread
+    constexpr int HT = (VP * ROWS + kMmaThreads - 1) / kMmaThreads;       // horizontal-sum tasks per thread
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // DB: the two region and candidate buffers are distinct LDS objects, so
+    // that the compiler sees that reads of one do not alias the LDS-DMA into
+    // the other (no vmcnt wait for the prefetch before them)
+    constexpr int RB = DB ? VP * VS : 16, CB = DB ? kMmaChunk * 8 : 16;
+    __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB], s_reg1[RB];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[CB];
+    __shared__ int s_ids[2];
+    __shared__ int s_V;
+    __shared__ double s_recip[65];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int V = sc.V;
+    const int npiece = V * RPV * 2;
+    if (tid <= 64) s_recip[tid] = c_recip.r[tid];
+    if (tid == 0) s_V = V;
+    const MmaLds L = mma_layout<WID, NBLK>(V);
+    uint32_t* htmp = (uint32_t*)(smem + L.sb);
+    int32_t* tsb = (int32_t*)(smem + L.sb);
+    double* tw = (double*)(smem + L.w);
+    float* twf = (float*)(smem + L.wf);
+    CandInfo* ci = (CandInfo*)(smem + L.ci) + wave * 16;
+    WaveSlot<NBLK>* wp = (WaveSlot<NBLK>*)(smem + L.wp) + wave;
+    if (tid < 8) ((uint32_t*)(smem + L.zero))[tid] = 0u;
+
+    const double kn = (double)NPX / (double)(NPX - 1);
+    const double tq = a.thr / kn;
+    const int n_units = t.item_off[t.ntiles];
+    int32_t* head = &t.tile_count[t.ntiles];
+    const int m = lane & 15, kh = lane >> 4;
+
+    // The region of an item (gv rows, signed bytes) goes to LDS by LDS-DMA
+    // (global_load_lds_dwordx4: 64 lanes x 16 B land contiguously), 32 B per
+    // region row and RPV rows per view including one pad row, so that the
+    // image is linear in the piece index; rows outside the image are clamped
+    // (their pixels are never inside a valid window).
+    auto region_buf = [&](int buf) -> uint8_t* { return DB ? (buf ? s_reg1 : s_reg0) : smem + L.reg; };
+    auto cand_buf = [&](int buf) -> uint8_t* { return DB ? (buf ? s_cand1 : s_cand0) : smem + L.cand; };
+    auto stage = [&](const int4 d, auto bufc) {
+        constexpr int buf = decltype(bufc)::value;
+        const int ty = d.x / t.ntx, tx = d.x - ty * t.ntx;
+        const int x0 = tx * MVS_TILE_W, yr0 = ty * MVS_TILE_H - WID;
+        uint8_t* base = region_buf(buf);
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int k = tid + p * kMmaThreads;
+            if (k < npiece) {
+                const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
+                const int y = min(max(yr0 + (r2 >> 1), 0), sc.H - 1);
+                const uint8_t* src = sc.gv + ((int64_t)v * sc.H + y) * sc.Wp + (x0 - 8) + 16 * (r2 & 1);
+                __builtin_amdgcn_global_load_lds((const void*)src,
+                                                 (void __attribute__((address_space(3)))*)(base + (p * kMmaThreads + wave * 64) * 16),
+                                                 16, 0, 0);
+            }
+        }
+        // the item's sorted (id, pk) entries, one dword per lane
+        uint8_t* cbase = cand_buf(buf);
+        const int32_t* csrc = (const int32_t*)(sorted + d.y);
+#pragma unroll
+        for (int p = 0; p < 2 * kMmaChunk / kMmaThreads; ++p) {
+            const int k = tid + p * kMmaThreads;
+            if (k < 2 * d.z)
+                __builtin_amdgcn_global_load_lds((const void*)(csrc + k),
+                                                 (void __attribute__((address_space(3)))*)(cbase + (p * kMmaThreads + wave * 64) * 4),
+                                                 4, 0, 0);
+        }
+    };
+
+    // Work items flow through a pipeline: while item k is scored, item k+1's
+    // region (DB) and candidate list, item k+2's descriptor and thread 0's
+    // claim of item k+3 are in flight; the barrier that ends item k retires them.
+    if (tid == 0) {
+        s_ids[0] = atomicAdd(head, 1);
+        s_ids[1] = atomicAdd(head, 1);
+    }
+    __syncthreads();
+    int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
+    int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
+    if (cur >= n_units) return;
+    int4 dcur = items[cur];
+    dcur = make_int4(__builtin_amdgcn_readfirstlane(dcur.x), __builtin_amdgcn_readfirstlane(dcur.y),
+                     __builtin_amdgcn_readfirstlane(dcur.z), 0);
+    stage(dcur, std::integral_constant<int, 0>{});
+    // item nx1's descriptor (uniform, scalar loads) and thread 0's claim of
+    // the item after it
+    int4 dnx1 = nx1 < n_units ? items[nx1] : make_int4(0, 0, 0, 0);
+    int pend = 0;
+    if (tid == 0) pend = atomicAdd(head, 1);
+    __syncthreads();   // everyone has read s_ids before they are rewritten
+
+    // one round per work item; the rounds alternate the buffers (DB), with the
+    // buffer index a compile-time constant in each
+    auto round = [&](auto bufc) -> bool {
+        constexpr int buf = decltype(bufc)::value;
+        STAMP(t0);
+        const int nc = dcur.z;
+            const uint8_t* reg = region_buf(buf);
+            const int2* cand = (const int2*)cand_buf(buf);
+            // ---- 1. this item's region and candidates are staged ----
+            if (tid == 0) s_ids[0] = pend;
+            __syncthreads();
+            const int nx2 = __builtin_amdgcn_readfirstlane(s_ids[0]);
+            STAMP(t1);
+            // thread -> (row, view) maps of phase 2, from a V read after the
+            // barrier (not hoisted: no registers held across phase 3)
+            const int Vl = s_V;
+            const int h_rho0 = tid / Vl, h_v0 = tid - h_rho0 * Vl;
+            const bool m2 = tid < Vl * 16;
+            // ---- 2. S_b and w of every view at the tile's pixels ----
+            // horizontal sums of each region row on the unsigned bytes g = s + 128
+            // (the moments are shift invariant): prefix sums by v_sad_u8 and
+            // v_dot4_u32_u8, packed as (sum g^2) << 12 | sum g
+    #pragma unroll
+            for (int j = 0; j < HT; ++j) {
+                if (tid + j * kMmaThreads < V * ROWS) {
+                    const int k = tid + j * kMmaThreads;
+                    const int rho = j ? k / Vl : h_rho0, v = j ? k - rho * Vl : h_v0;
+                    const uint4 lo = *(const uint4*)(reg + v * VS + rho * 32);
+                    const uint4 hi = *(const uint4*)(reg + v * VS + rho * 32 + 16);
+                    const uint32_t d[8] = {lo.x ^ 0x80808080u, lo.y ^ 0x80808080u, lo.z ^ 0x80808080u,
+                                           lo.w ^ 0x80808080u, hi.x ^ 0x80808080u, hi.y ^ 0x80808080u,
+                                           hi.z ^ 0x80808080u, hi.w ^ 0x80808080u};
+                    uint32_t PS[33], PQ[33];
+                    PS[0] = 0;
+                    PQ[0] = 0;
+    #pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t m1 = d[k] & 0xffu, m2b = d[k] & 0xffffu, m3 = d[k] & 0xffffffu;
+                        PS[4 * k + 1] = __builtin_amdgcn_sad_u8(m1, 0u, PS[4 * k]);
+                        PS[4 * k + 2] = __builtin_amdgcn_sad_u8(m2b, 0u, PS[4 * k]);
+                        PS[4 * k + 3] = __builtin_amdgcn_sad_u8(m3, 0u, PS[4 * k]);
+                        PS[4 * k + 4] = __builtin_amdgcn_sad_u8(d[k], 0u, PS[4 * k]);
+                        PQ[4 * k + 1] = __builtin_amdgcn_udot4(m1, d[k], PQ[4 * k], false);
+                        PQ[4 * k + 2] = __builtin_amdgcn_udot4(m2b, d[k], PQ[4 * k], false);
+                        PQ[4 * k + 3] = __builtin_amdgcn_udot4(m3, d[k], PQ[4 * k], false);
+                        PQ[4 * k + 4] = __builtin_amdgcn_udot4(d[k], d[k], PQ[4 * k], false);
+                    }
+                    uint32_t* hrow = htmp + rho * 16 * VP + v;
+    #pragma unroll
+                    for (int x = 0; x < 16; ++x)
+                        hrow[x * VP] = ((PQ[x + C0 + NB] - PQ[x + C0]) << 12) | (PS[x + C0 + NB] - PS[x + C0]);
+                }
+            }
+            __syncthreads();
+            STAMP(t1a);
+            // vertical sums -> (S_b of s, w) per (pixel, view); the table overwrites
+            // the horizontal sums, so every thread reads first
+            int ms[MVS_TILE_H];
+            double mw[MVS_TILE_H];
+            const int m2x = h_rho0, m2v = h_v0;   // thread -> (pixel column, view)
+            if (m2) {
+                int S[ROWS], Q[ROWS];
+    #pragma unroll
+                for (int rho = 0; rho < ROWS; ++rho) {
+                    const uint32_t h = htmp[(rho * 16 + m2x) * VP + m2v];
+                    S[rho] = (int)(h & 0xfffu);
+                    Q[rho] = (int)(h >> 12);
+                }
+                int sg = 0, q = 0;
+    #pragma unroll
+                for (int rho = 0; rho < NB; ++rho) {
+                    sg += S[rho];
+                    q += Q[rho];
+                }
+    #pragma unroll
+                for (int y = 0; y < MVS_TILE_H; ++y) {
+                    if (y > 0) {
+                        sg += S[y + NB - 1] - S[y - 1];
+                        q += Q[y + NB - 1] - Q[y - 1];
+                    }
+                    const int db = NPX * q - sg * sg;   // < 2^31: n * sum g^2 <= 121 * 121 * 255^2
+                    double w = __builtin_nan("");       // constant window: ctNcc's nan
+                    if (db > 0) {
+                        const double D = (double)db;
+                        w = __builtin_amdgcn_rsq(D);
+                        w = w * (1.5 - 0.5 * D * w * w);
+                        w = w * (1.5 - 0.5 * D * w * w);
+                    }
+                    ms[y] = sg - 128 * NPX;             // S_b of s = g - 128
+                    mw[y] = w;
+                }
+            }
+            __syncthreads();
+            STAMP(t1b);
+            if (m2)
+    #pragma unroll
+                for (int y = 0; y < MVS_TILE_H; ++y) {
+                    const int o = (y * 16 + m2x) * VP + m2v;
+                    tsb[o] = ms[y];
+                    tw[o] = mw[y];
+                    if constexpr (WF) twf[o] = (float)mw[y];
+                }
+            if (VP > V)   // views V..VP-1 of the last 16-view block: never pass
+                for (int k = tid; k < 128 * (VP - V); k += kMmaThreads) {
+                    const int px = k / (VP - V), v = V + (k - px * (VP - V));
+                    tsb[px * VP + v] = 0;
+                    tw[px * VP + v] = __builtin_nan("");
+                    if constexpr (WF) twf[px * VP + v] = __builtin_nanf("");
+                }
+            __syncthreads();
+            STAMP(t2);
+            // the next items' loads, in flight during phase 3 (phase 2's register
+            // spills would otherwise wait for them: vmcnt retires in order): item
+            // nx1's region and candidates (DB), item nx2's descriptor (scalar
+            // loads) and thread 0's claim of the item after it
+            if (nx1 < n_units) {
+                if constexpr (DB) stage(dnx1, std::integral_constant<int, buf ^ 1>{});
+            }
+            int4 dnx2 = make_int4(0, 0, 0, 0);
+            if (nx2 < n_units) {
+                dnx2 = items[nx2];
+                if (tid == 0) pend = atomicAdd(head, 1);
+            }
+    
+            // ---- 3. + 4. the candidates, 16 per wave and M-block ----
+            const int nblk = (nc + 15) >> 4;
+    #ifdef MVS_STAMPS
+            unsigned long long w0blk = 0;
+    #endif
+            for (int blk = wave; blk < nblk; blk += kMmaWaves) {
+    #ifdef MVS_STAMPS
+                ++w0blk;
+    #endif
+                const int kk = blk * 16 + m;
+                const bool valid = kk < nc;
+                const int2 e = valid ? cand[kk] : make_int2(-1, 0);
+                const int qrel = e.y & 15, rrel = (e.y >> 4) & 7, R = e.y >> 7;
+                // A: the reference window, masked to candidate m's window columns
+                // (this lane's 16 columns) and rows (K-step rows in the window)
+                const uint32_t wm = valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u;
+                const uint32_t hm = wm >> (16 * (kh & 1));
+                uint32_t cm[4];
+    #pragma unroll
+                for (int k4 = 0; k4 < 4; ++k4) cm[k4] = byte_mask((hm >> (4 * k4)) & 15u);
+                const uint32_t rb = valid ? (((1u << NB) - 1u) << rrel) >> (kh >> 1) : 0u;
+                const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
+                const uint8_t* aptr = reg + R * VS + lofs;
+                const uint8_t* bptr[NBLK];
+    #pragma unroll
+                for (int nb = 0; nb < NBLK; ++nb) bptr[nb] = reg + min(16 * nb + m, V - 1) * VS + lofs;
+                v4i C[NBLK];
+    #pragma unroll
+                for (int nb = 0; nb < NBLK; ++nb) C[nb] = (v4i){0, 0, 0, 0};
+    #pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const bool rv = (rb >> (2 * s)) & 1u;
+                    const uint4 av = rv ? *(const uint4*)(aptr + 64 * s) : make_uint4(0u, 0u, 0u, 0u);
+                    const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]),
+                                   (int)(av.w & cm[3])};
+    #pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) {
+                        const uint4 bv = *(const uint4*)(bptr[nb] + 64 * s);
+                        const v4i B = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
+                        C[nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, C[nb], 0, 0, 0);
+                    }
+                }
+                // candidate m's constants (row 0 of the wave), shared through LDS
+                double my_ca = 0.0;
+                if (kh == 0) {
+                    CandInfo c;
+                    c.px = e.y & 127;                    // rrel * 16 + qrel
+                    const int o = c.px * VP + R;
+                    const double wa = tw[o];
+                    c.R = valid ? R : -1;
+                    c.Sa = -tsb[o];                      // -S_a: num = n C + (-S_a) S_b
+                    c.idx = e.x;
+                    c.T = valid ? (float)(tq / wa) : __builtin_nanf("");
+                    c.gT = 2e-6f * fabsf(c.T);
+                    c.ca = kn * wa;
+                    ci[m] = c;
+                    my_ca = c.ca;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // lane (kh, m) holds C[4 kh + i][16 nb + m]: candidate 4 kh + i, view 16 nb + m
+                uint32_t pmv = 0, gdv = 0;
+                double sacc[4];
+                static_for<4>([&](auto Ic) {
+                    constexpr int i = Ic;
+                    const CandInfo c = ci[4 * kh + i];
+                    double sa = 0.0;
+                    uint64_t g = 0;
+                    static_for<NBLK>([&](auto Nc) {
+                        constexpr int nb = Nc;
+                        const int vl = 16 * nb + m;
+                        const int o = c.px * VP + vl;
+                        const int num = __mul24(c.Sa, tsb[o]) + __mul24(NPX, C[nb][i]);
+                        const double w = tw[o];
+                        // lane masks straight from v_cmp (a ballot of a bool would
+                        // round-trip it through a VGPR)
+                        const uint64_t liv = __builtin_amdgcn_uicmp((uint32_t)vl, (uint32_t)c.R, 33);   // ne
+                        bool pass;
+                        uint64_t P;
+                        if constexpr (FAST) {
+                            // ncc > thr <=> num w_b > T; w_b nan (constant window) never passes
+                            const float wf = WF ? twf[o] : (float)w;
+                            const float x = fmaf((float)num, wf, -c.T);
+                            pass = vl != c.R && x > 0.0f;
+                            P = __builtin_amdgcn_fcmpf(x, 0.0f, 2) & liv;                   // ogt
+                            g |= __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4) & liv;           // olt
+                        } else {
+                            const double ncc = (double)num * w * c.ca;
+                            pass = vl != c.R && ncc > a.thr;
+                            P = __ballot(pass);
+                            g |= __ballot(vl != c.R && fabs(ncc - a.thr) <= kGuard);
+                        }
+                        pmv = writelane<2 * (i * NBLK + nb)>(pmv, (uint32_t)P);
+                        pmv = writelane<2 * (i * NBLK + nb) + 1>(pmv, (uint32_t)(P >> 32));
+                        sa = fma((double)num, pass ? w : 0.0, sa);
+                    });
+                    gdv = writelane<2 * i>(gdv, (uint32_t)g);
+                    gdv = writelane<2 * i + 1>(gdv, (uint32_t)(g >> 32));
+                    sacc[i] = sa;
+                });
+                if (lane < 2 * 4 * NBLK) wp->pm[lane] = pmv;
+                if (lane < 8) wp->gd[lane] = gdv;
+                if (a.avg != nullptr) {
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) sacc[i] = row_sum16(sacc[i]);
+                    const double mine = m == 0 ? sacc[0] : m == 1 ? sacc[1] : m == 2 ? sacc[2] : sacc[3];
+                    if (m < 4) wp->wsum[4 * kh + m] = mine;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (kh == 0 && valid) {
+                    // candidate m = 4 j + i: 16 bits j of ballot (i, nb) -> bits 16 nb of its mask
+                    const int j = m >> 2, i = m & 3;
+                    const uint16_t* pm16 = (const uint16_t*)wp->pm;
+                    uint64_t mk = 0;
+    #pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) mk |= (uint64_t)pm16[4 * (i * NBLK + nb) + j] << (16 * nb);
+                    const uint32_t gg = ((const uint16_t*)wp->gd)[4 * i + j];
+                    const int cnt = __popcll(mk);
+                    const int64_t idx = e.x;
+                    a.mask[idx] = mk;
+                    a.count[idx] = cnt;
+                    if (a.avg) a.avg[idx] = cnt ? wp->wsum[m] * my_ca * s_recip[cnt] : 0.0;
+                    if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
+                }
+            }
+            STAMP(t3);
+            __syncthreads();
+            STAMP(t4);
+            STAMP_ADD(0, 1);
+            STAMP_ADD(1, t1 - t0);
+            STAMP_ADD(2, t2 - t1);
+            STAMP_ADD(3, t4 - t2);
+            STAMP_ADD_W0(4, t3 - t2);
+            STAMP_ADD_W0(5, w0blk);
+            STAMP_ADD(6, t1a - t1);
+            STAMP_ADD(7, t1b - t1a);
+        if (nx1 >= n_units) return false;
+        if constexpr (!DB) stage(dnx1, std::integral_constant<int, 0>{});   // the buffer is free now; lands by the next barrier
+        cur = nx1;
+        dcur = dnx1;
+        nx1 = nx2;
+        dnx1 = dnx2;
+        return true;
+    };
+    for (;;) {
+        if (!round(std::integral_constant<int, 0>{})) break;
+        if (!round(std::integral_constant<int, DB ? 1 : 0>{})) break;
     }
 }
 
@@ -1198,16 +1695,42 @@ int launch_score_w(const SceneDev* sc, const ScoreArgs* a, hipStream_t s, hipEve
 
 template <int WID, int NBLK, bool GROUPED>
 int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s) {
-    const MmaLds L = mma_lds<WID>(GROUPED ? kGroupViews : sc->V, 16 * NBLK, GROUPED);
     static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)k_score_mma<WID, NBLK, GROUPED>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, L.total) != hipSuccess)
-            return -1;
-        attr = true;
+    if constexpr (GROUPED) {
+        const MmaLdsG L = mma_lds_g<WID>(kGroupViews, 16 * NBLK, true);
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)k_score_mma_g<WID, NBLK, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, L.total) != hipSuccess)
+                return -1;
+            attr = true;
+        }
+        hipLaunchKernelGGL((k_score_mma_g<WID, NBLK, true>), dim3(kMmaGrid), dim3(kMmaThreads), L.total, s,
+                           *sc, *a, *t);
+    } else {
+        // the largest table is sized for V = 16 NBLK; every V of this NBLK fits in it
+        const int lds = mma_layout<WID, NBLK>(16 * NBLK).total;
+        const int used = mma_layout<WID, NBLK>(sc->V).total;
+        if (fabs(a->thr) >= 0.01) {
+            if (!attr) {
+                if (hipFuncSetAttribute((const void*)k_score_mma<WID, NBLK, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+                    return -1;
+                attr = true;
+            }
+            hipLaunchKernelGGL((k_score_mma<WID, NBLK, true>), dim3(kMmaGrid), dim3(kMmaThreads), used, s, *sc, *a,
+                               *t, (const int4*)t->items, (const int2*)t->sorted);
+        } else {
+            static bool attr_slow = false;
+            if (!attr_slow) {
+                if (hipFuncSetAttribute((const void*)k_score_mma<WID, NBLK, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+                    return -1;
+                attr_slow = true;
+            }
+            hipLaunchKernelGGL((k_score_mma<WID, NBLK, false>), dim3(kMmaGrid), dim3(kMmaThreads), used, s, *sc,
+                               *a, *t, (const int4*)t->items, (const int2*)t->sorted);
+        }
     }
-    hipLaunchKernelGGL((k_score_mma<WID, NBLK, GROUPED>), dim3(kMmaGrid), dim3(kMmaThreads), L.total, s,
-                       *sc, *a, *t);
     return 0;
 }
 
@@ -1278,6 +1801,12 @@ int grid_for(int64_t n, int block, int cap) {
 
 }  // namespace
 
+#ifdef MVS_STAMPS
+extern "C" int mvs_read_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int mvs_launch_build_scene(const SceneDev* sc, const uint8_t* d_rgb, uint8_t* d_stack,
                                       uint8_t* d_gv_base, hipStream_t s) {
     (void)d_gv_base;
@@ -1298,16 +1827,24 @@ extern "C" int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid,
     }
 }
 
+template <int WID>
+size_t mma_lds_bytes_w(int V) {
+    if (V > kGroupViews) return (size_t)mma_lds_g<WID>(kGroupViews, 64, true).total;
+    switch ((V + 15) / 16) {
+        case 1: return (size_t)mma_layout<WID, 1>(V).total;
+        case 2: return (size_t)mma_layout<WID, 2>(V).total;
+        case 3: return (size_t)mma_layout<WID, 3>(V).total;
+        default: return (size_t)mma_layout<WID, 4>(V).total;
+    }
+}
+
 extern "C" size_t mvs_mma_lds_bytes(int V, int wid) {
-    const bool grouped = V > kGroupViews;
-    const int VR = grouped ? kGroupViews : V;
-    const int VP = grouped ? 64 : 16 * ((V + 15) / 16);
     switch (wid) {
-        case 1: return (size_t)mma_lds<1>(VR, VP, grouped).total;
-        case 2: return (size_t)mma_lds<2>(VR, VP, grouped).total;
-        case 3: return (size_t)mma_lds<3>(VR, VP, grouped).total;
-        case 4: return (size_t)mma_lds<4>(VR, VP, grouped).total;
-        case 5: return (size_t)mma_lds<5>(VR, VP, grouped).total;
+        case 1: return mma_lds_bytes_w<1>(V);
+        case 2: return mma_lds_bytes_w<2>(V);
+        case 3: return mma_lds_bytes_w<3>(V);
+        case 4: return mma_lds_bytes_w<4>(V);
+        case 5: return mma_lds_bytes_w<5>(V);
         default: return 0;
     }
 }

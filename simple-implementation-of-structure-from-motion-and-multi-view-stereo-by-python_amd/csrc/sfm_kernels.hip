@@ -14,7 +14,7 @@ DEV int refl101(int i, int n) {     // BORDER_REFLECT_101 for overruns of <= n -
 }
 
 DEV float gv_px(const SceneDev& sc, int v, int y, int x) {
-    return (float)sc.gv[((int64_t)v * sc.H + y) * sc.Wp + x];
+    return (float)(sc.gv[((int64_t)v * sc.H + y) * sc.Wp + x] ^ 0x80u);   // gv holds g - 128
 }
 
 // Sobel(ksize 3, scale 1/8) at (y, x): the scale is folded into the smoothing
@@ -183,7 +183,7 @@ __global__ void k_gather_desc(const SceneDev sc, int v, const int32_t* __restric
             for (int b = 0; b < 4; ++b) {
                 const int p = 4 * k + b;
                 if (p < npx) {
-                    const uint32_t g = sc.gv[((int64_t)v * sc.H + r - wid + p / nb) * sc.Wp + q - wid + p % nb];
+                    const uint32_t g = sc.gv[((int64_t)v * sc.H + r - wid + p / nb) * sc.Wp + q - wid + p % nb] ^ 0x80u;
                     wd |= g << (8 * b);
                     s += (int32_t)g;
                     ss += (int32_t)(g * g);
