@@ -1,19 +1,38 @@
 """Benchmark: candidate patches NCC-scored per second (BASELINE.json metric).
 
-Workload (BASELINE configs[1]): the real dinoRing
+Headline (BASELINE configs[1]): the real dinoRing
 gray stack (48 views x 640x480, data/dinoRing), one expansion sweep = a batch
-of 2^20 synthetic candidate patches per GPU (reference view, sub-pixel pixel,
-depth 0.60-0.72 m; seed 0 + rank), every candidate photo-tested against all 48
-views with the reference's 11x11 window (wid=5, MVS2.py:64/69) at MIN_NCC 0.7.
-A step = score the sweep on the GPU (inputs resident in HBM) + compact the
-accepted candidates (|V| >= 3: accept bitmap + their V masks) + RCCL
-all-gather of that accepted set across ranks (the sweep's exchange step;
-skipped at N=1).
+of 2^20 candidate patches per GPU (reference view, sub-pixel pixel, depth
+0.60-0.72 m), every candidate photo-tested against all 48 views with the
+reference's 11x11 window (wid=5, MVS2.py:64/69) at MIN_NCC 0.7.  The sweep is
+one block of a global candidate queue: rank r scores block r (seed r) of a
+queue of N x 2^20 candidates (weak scaling), or with --strong its
+shard_range slice of one 2^20 queue.  A step = score the sweep on the GPU
+(inputs resident in HBM) + the sweep's exchange: the accepted candidates
+(|V| >= 3) with their masks and 3D points all-gathered over RCCL (N > 1).
+
+Beside the headline (rank 0 at N = 1 only, so that the driver's N > 1 runs
+stay short):
+  roofline     the binding roof of the dominant kernel (k_score_mma) from the
+               live kernel time and the per-launch counters of the committed
+               rocprofv3 PMC profile (profiles/r02/pmc.json): HBM bytes,
+               VALU-busy cycles, MFMA i8 operations; frac <= 1 each
+  cold_sweep   scene setup from the resident images (k_build_scene) + the sweep
+  secondary    wid 3 (BASELINE config 2's 7x7 window)
+  stage        the whole reference stage: DensePointsWithMVS2 on dinoRing +
+               tests/golden/seeds_dino.npz with the reference's 100,000-pop cap
+               (MVS2.py:321), wall time, reference-equivalent tests/s, phase
+               times, rows checked against the oracle fixture's sha256
+  ring256      SURVEY 8(d) config 4: 256 views of 1920x1080 (a textured sphere,
+               rendered on the GPU so that sweeps accept candidates), 2^20
+               candidates per sweep, view-group scorer
+  cpu_baseline the oracle (C port of the reference arithmetic) on the host cores
 
 python bench.py [--gpus N --steps K --warmup W --n CANDS --wid 5]
 N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import hashlib
 import importlib
 import json
 import os
@@ -26,11 +45,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 PKG_NAME = "simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd"
 sys.path.insert(0, REPO)
 
-PEAK_HBM = 8.0e12          # MI355X HBM3E peak, B/s (MI355X_MICROARCH.md)
-KERNEL_NAME = {"auto": "k_score_tiled3", "tiled": "k_score_tiled3", "direct": "k_score"}  # variant 10 A/B only; the default is k_score_tiled5
+PEAK_HBM = 8.0e12          # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
+PEAK_I8 = 5.0e15           # dense i8 MFMA ops/s (2x the 2.5 PF dense bf16; no sparsity)
+SIMDS = 1024               # 256 CUs x 4 SIMDs
+CLOCK = 2.4e9              # peak engine clock, Hz
+PMC_PATH = os.path.join(REPO, "profiles", "r02", "pmc.json")
 
 
-def algorithmic_bytes(V, wid):
+def logical_bytes(V, wid):
     """V*(2w+1)^2 window bytes + 32 B in + 8*ceil(V/64) + 16 B out."""
     return V * (2 * wid + 1) ** 2 + 32 + 8 * ((V + 63) // 64) + 16
 
@@ -50,6 +72,59 @@ def load_scene():
     return rgb, np.array(K), np.array(R), np.array(t)
 
 
+def pmc_entry(scene, V, wid, n):
+    """Per-launch counters of the scorer for this configuration from the
+    committed PMC profile, or None."""
+    if not os.path.exists(PMC_PATH):
+        return None
+    try:
+        for e in json.load(open(PMC_PATH))["entries"]:
+            if (e["scene"], e["V"], e["wid"], e["n"]) == (scene, V, wid, n):
+                return e
+    except Exception:
+        return None
+    return None
+
+
+def roofline(entry, V, wid, n, kms):
+    """Roofs of the dominant kernel: measured HBM bytes, VALU-busy cycles and
+    MFMA i8 operations per launch (PMC) over the live launch time.  The binding
+    roof is the one with the largest fraction; each frac <= 1 because a unit
+    cannot be busier than its peak."""
+    npx = (2 * wid + 1) ** 2
+    out = {"kernel": entry["kernel"] if entry else "k_score_mma", "kernel_ms": kms,
+           "candidates_per_launch": n, "logical_bytes_per_candidate": logical_bytes(V, wid),
+           "logical_GBps": logical_bytes(V, wid) * n / (kms * 1e-3) / 1e9,
+           "logical_note": "SURVEY 8(d) bytes (every candidate's V windows read once); the scorer "
+                           "stages each tile's region once, so this is not a traffic figure"}
+    roofs = {}
+    useful = 2.0 * V * npx * n        # the window products sum s_R s_v of all V views
+    roofs["mfma_useful"] = {"achieved": useful / (kms * 1e-3) / 1e12, "peak": PEAK_I8 / 1e12,
+                            "unit": "TOP/s (i8, useful window products)"}
+    traffic = None
+    if entry:
+        c = entry["per_launch"]
+        traffic = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+        roofs["hbm"] = {"achieved": traffic / (kms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                        "bytes_per_launch": traffic}
+        valu = c["SQ_ACTIVE_INST_VALU"] * 4.0            # quad-cycles -> cycles, summed over SIMDs
+        roofs["valu"] = {"achieved": valu / (kms * 1e-3) / 1e9, "peak": SIMDS * CLOCK / 1e9,
+                         "unit": "G SIMD-busy-cycles/s",
+                         "pmc_self_frac": valu / (SIMDS * c["GRBM_GUI_ACTIVE"] / 8.0)}
+        if "SQ_INSTS_VALU_MFMA_I8" in c:
+            ops = c["SQ_INSTS_VALU_MFMA_I8"] * 16 * 16 * 64 * 2.0
+            roofs["mfma_issued"] = {"achieved": ops / (kms * 1e-3) / 1e12, "peak": PEAK_I8 / 1e12,
+                                    "unit": "TOP/s (i8, issued)"}
+    for r in roofs.values():
+        r["frac"] = r["achieved"] / r["peak"]
+    bound = max(roofs, key=lambda k: roofs[k]["frac"])
+    b = roofs[bound]
+    out.update({"bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"],
+                "frac": b["frac"], "traffic": traffic, "roofs": roofs,
+                "source": os.path.relpath(PMC_PATH, REPO) if entry else None})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,6 +134,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=1 << 20, help="candidates per GPU per sweep")
+    ap.add_argument("--strong", action="store_true",
+                    help="one queue of --n candidates split over the ranks (default: --n per rank)")
     ap.add_argument("--wid", type=int, default=5)
     ap.add_argument("--thr", type=float, default=0.7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -66,18 +143,14 @@ def main():
                     help="candidates the single-threaded oracle scores (~10 s)")
     ap.add_argument("--secondary-wid", type=int, default=3)
     ap.add_argument("--no-stage", action="store_true", help="skip the full-stage secondary")
-    ap.add_argument("--kernel", choices=["auto", "direct", "tiled"], default="auto",
-                    help="scoring kernel (MVS_SCORE_KERNEL)")
+    ap.add_argument("--no-ring", action="store_true", help="skip the ring256 secondary")
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
-                    help="dino: dinoRing 48x640x480 (SURVEY 8(d) config 2, the headline); "
-                         "ring256: synthetic 256x1920x1080 uniform-random textures (config 4)")
+                    help="headline scene (ring256: config 4 as the headline, for profiling)")
     a = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
-    if a.kernel != "auto":
-        os.environ["MVS_SCORE_KERNEL"] = a.kernel
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
@@ -90,165 +163,206 @@ def main():
             dist.init_process_group("gloo")
     pkg = importlib.import_module(PKG_NAME)
     par = importlib.import_module(PKG_NAME + ".parallel")
+    syn = pkg.synthetic
 
-    if a.scene == "dino":
-        rgb, K, R, t = load_scene()
-    else:
-        rgb, K, R, t = pkg.synthetic.ring_scene(256, 1080, 1920, seed=0)
+    def make_scene(which):
+        if which == "dino":
+            return load_scene()
+        return syn.sphere_scene_device(256, 1080, 1920, seed=0, device=dev)
+
+    rgb, K, R, t = make_scene(a.scene)
     V, H, W = rgb.shape[0], rgb.shape[1], rgb.shape[2]
     ctx = pkg.MvsContext(rgb, K, R, t, device=local)
-    c_np, ref_np = pkg.synthetic.candidates(a.n, K, R, t, W=W, H=H, seed=rank)
-    c = torch.from_numpy(c_np).to(dev)
-    ref = torch.from_numpy(ref_np).to(dev)
-    n = a.n
-    words = (V + 63) // 64
-    xy = torch.empty((n, 2), dtype=torch.float64, device=dev)
-    mask = torch.empty((n, words), dtype=torch.int64, device=dev)
-    count = torch.empty(n, dtype=torch.int32, device=dev)
-    avg = torch.empty(n, dtype=torch.float64, device=dev)
     vlb = 3 if V > 2 else 2
     stream = torch.cuda.Stream(dev)          # the scoring kernels run on THIS stream
     torch.cuda.synchronize()
     torch.cuda.set_stream(stream)
-    gathered = {"n": 0}
 
-    def step(wid, evs=None):
-        if evs is not None:
-            evs[0].record(stream)
-        ctx.score_device(c, ref, xy, mask, count, avg, a.thr, wid, stream=stream.cuda_stream)
-        if evs is not None:
-            evs[1].record(stream)
-        if world > 1:
-            # the sweep's exchange (parallel.py): every rank's accepted set
-            # (accept bitmap + V masks; count = popcount, centroids known) to every rank
-            blocks = par.exchange_accepted(count, mask, vlb)
-            gathered["n"] = sum((b.numel() - 1 - (n + 63) // 64) // words for b in blocks)
+    def sweep_inputs(ctx_V, Kc, Rc, tc, Wc, Hc, n_local, strong):
+        """This rank's block of the global candidate queue (device tensors)."""
+        if strong:
+            b, e = par.shard_range(a.n, rank, world)
+            c_np, ref_np = syn.candidates(a.n, Kc, Rc, tc, W=Wc, H=Hc, seed=0)
+            c_np, ref_np, off = c_np[b:e], ref_np[b:e], b
+        else:
+            c_np, ref_np = syn.candidates(n_local, Kc, Rc, tc, W=Wc, H=Hc, seed=rank)
+            off = rank * n_local
+        n = len(ref_np)
+        return {"c_np": c_np, "ref_np": ref_np, "off": off, "n": n,
+                "c": torch.from_numpy(np.ascontiguousarray(c_np)).to(dev),
+                "ref": torch.from_numpy(np.ascontiguousarray(ref_np)).to(dev),
+                "xy": torch.empty((n, 2), dtype=torch.float64, device=dev),
+                "mask": torch.empty((n, (ctx_V + 63) // 64), dtype=torch.int64, device=dev),
+                "count": torch.empty(n, dtype=torch.int32, device=dev),
+                "avg": torch.empty(n, dtype=torch.float64, device=dev)}
 
-    def timed(wid, steps, warmup):
+    def timed(cx, sw, wid, steps, warmup, exchange=True, rebuild=False):
+        """steps timed sweeps -> (wall s (max over ranks), kernel ms per launch,
+        score-call ms, records exchanged in the last step)."""
+        got = {"n": 0}
+
+        def step(evs=None):
+            if evs is not None:
+                evs[0].record(stream)
+            if rebuild:
+                cx.rebuild(stream=stream.cuda_stream)
+            cx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], a.thr, wid,
+                            stream=stream.cuda_stream)
+            if evs is not None:
+                evs[1].record(stream)
+            if exchange and world > 1:
+                rec = par.exchange_accepted_points(sw["off"], sw["count"], sw["mask"], sw["c"], vlb)
+                got["n"] = int(rec.shape[0])
+
         for _ in range(warmup):
-            step(wid)
+            step()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(steps)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        ctx.kernel_timing(True)     # HIP events around the dominant kernel, on its stream
+        cx.kernel_timing(True)     # HIP events around the dominant kernel, on its stream
         t0 = time.perf_counter()
         for k in range(steps):
-            step(wid, evs[k])
+            step(evs[k])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        ctx.kernel_timing(False)
-        kt, kl = ctx.kernel_time()
+        cx.kernel_timing(False)
+        kt, kl = cx.kernel_time()
         if kl != steps or kt <= 0.0:
             raise RuntimeError(f"kernel timing recorded {kl} launches / {kt} ms for {steps} steps")
-        kms = kt / kl                                                    # dominant kernel
-        pms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / steps   # whole scoring call
+        pms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / steps
         if world > 1:
             tt = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
-        return dt, kms, pms
+        return dt, kt / kl, pms, got["n"]
 
-    dt, kms, pms = timed(a.wid, a.steps, a.warmup)
-    total = n * world * a.steps
-    value = total / dt
-    B = algorithmic_bytes(V, a.wid)
-    achieved = B * n / (kms * 1e-3)
-    accepted = int((count >= vlb).sum().item())
-    sec = None
-    if a.secondary_wid and a.secondary_wid != a.wid:
-        dt2, kms2, _ = timed(a.secondary_wid, max(a.steps // 2, 5), 2)
-        B2 = algorithmic_bytes(V, a.secondary_wid)
-        sec = {"wid": a.secondary_wid, "value": n * world * max(a.steps // 2, 5) / dt2,
-               "kernel_ms": kms2, "achieved_GBps": B2 * n / (kms2 * 1e-3) / 1e9}
+    sw = sweep_inputs(V, K, R, t, W, H, a.n, a.strong)
+    n = sw["n"]
+    total_n = a.n if a.strong else a.n * world
+    dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup)
+    value = total_n * a.steps / dt
+    accepted = int((sw["count"] >= vlb).sum().item())
+    kernel_name = ctx.timed_kernel()
+    solo = rank == 0 and world == 1
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(REPO))
+    out = {
+        "metric": ("candidate patches/sec NCC-scored (640×480, 48 views) at 1/2/4/8 MI355X; % HBM roofline"
+                   if a.scene == "dino" else
+                   "candidate patches/sec NCC-scored (1920×1080, 256 views, synthetic) at 1/2/4/8 MI355X"),
+        "value": value,
+        "unit": "candidates/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong" if a.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": ("real dinoRing images (data/dinoRing)" if a.scene == "dino" else
+                 "synthetic textured sphere rendered on the GPU (seed 0)") +
+                " + synthetic candidate patches (global queue, block per rank)",
+        "config": {"workload": f"{'dinoRing' if a.scene == 'dino' else 'sphere ring'} {V}x{W}x{H}, "
+                               f"one expansion sweep of {n} candidates per GPU, "
+                               f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
+                               f"MIN_NCC {a.thr}, accepted records (with 3D points) all-gathered",
+                   "global_batch": total_n, "wid": a.wid, "views": V,
+                   "parallelism": f"candidate-queue shards x{world} (RCCL all-gather of accepted points)"},
+        "kernel": kernel_name,
+        "score_call_ms": pms,
+        "accepted_per_sweep": accepted,
+        "gathered_records": gathered,
+    }
+    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n), V, a.wid, n, kms)
+
+    if solo:
+        # cold sweep: scene setup from the resident images + the sweep
+        steps_c = max(a.steps // 5, 5)
+        cdt, _, cpms, _ = timed(ctx, sw, a.wid, steps_c, 1, exchange=False, rebuild=True)
+        out["cold_sweep"] = {"value": n * steps_c / cdt, "unit": "candidates/s",
+                             "ms_per_step": cdt / steps_c * 1e3, "setup_plus_score_call_ms": cpms,
+                             "note": "k_build_scene (RGB -> gray stack + signed view-major copy) "
+                                     "before every sweep; the warm figure is `value`"}
+        if a.secondary_wid and a.secondary_wid != a.wid:
+            s2 = max(a.steps // 2, 5)
+            dt2, kms2, pms2, _ = timed(ctx, sw, a.secondary_wid, s2, 2, exchange=False)
+            out["secondary"] = {"wid": a.secondary_wid, "value": n * s2 / dt2, "kernel_ms": kms2,
+                                "score_call_ms": pms2,
+                                "roofline": roofline(pmc_entry(a.scene, V, a.secondary_wid, n), V,
+                                                     a.secondary_wid, n, kms2)}
+
+    if solo and a.scene == "dino" and not a.no_stage:
+        sd = dict(np.load(os.path.join(REPO, "tests", "golden", "seeds_dino.npz")))
+        fx = json.load(open(os.path.join(REPO, "tests", "golden", "stage_oracle_cap100000.json")))
+        ctx.stage(sd["track_off"], sd["obs_view"], sd["obs_xy"], cell_size=2, scale=10.0, wid=5,
+                  max_pops=2000)                                       # warm
+        walls = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            ini, allp, st = ctx.stage(sd["track_off"], sd["obs_view"], sd["obs_xy"], cell_size=2,
+                                      scale=10.0, wid=5, max_pops=100000)
+            walls.append(time.perf_counter() - t0)
+        ok = (hashlib.sha256(np.ascontiguousarray(ini, "<f8").tobytes()).hexdigest() == fx["sha256_initial"]
+              and hashlib.sha256(np.ascontiguousarray(allp, "<f8").tobytes()).hexdigest() == fx["sha256_all"])
+        w = min(walls)
+        out["stage"] = {"workload": "DensePointsWithMVS2 (MVS2.py:176-295) on dinoRing + seeds_dino.npz, "
+                                    "100,000 pops (MVS2.py:321), wid 5, cell 2, scale 10",
+                        "wall_s": w, "wall_s_runs": walls, "pops": st["pops"],
+                        "reference_equivalent_tests": st["tests"],
+                        "tests_per_s": st["tests"] / w, "gpu_scored_candidates": st["scored"],
+                        "sweeps": st["sweeps"], "patches": len(allp), "initial_patches": len(ini),
+                        "phases_s": st["times"], "rows_match_oracle_fixture": bool(ok)}
+
+    if solo and a.scene == "dino" and not a.no_ring:
+        rrgb, rK, rR, rt = make_scene("ring256")
+        rV, rH, rW = rrgb.shape[:3]
+        rctx = pkg.MvsContext(rrgb, rK, rR, rt, device=local)
+        del rrgb
+        rsw = sweep_inputs(rV, rK, rR, rt, rW, rH, a.n, False)
+        s3 = max(a.steps // 5, 5)
+        rdt, rkms, rpms, _ = timed(rctx, rsw, a.wid, s3, 2, exchange=False)
+        out["ring256"] = {"workload": f"SURVEY 8(d) config 4: {rV} views x {rW}x{rH} (textured sphere), "
+                                      f"{rsw['n']} candidates per sweep, wid {a.wid}, MIN_NCC {a.thr}",
+                          "value": rsw["n"] * s3 / rdt, "unit": "candidates/s", "kernel": rctx.timed_kernel(),
+                          "kernel_ms": rkms, "score_call_ms": rpms,
+                          "accepted_per_sweep": int((rsw["count"] >= 3).sum().item()),
+                          "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"]), rV, a.wid,
+                                               rsw["n"], rkms)}
+        rctx.close()
+
+    if solo and not a.no_cpu_baseline:
         from oracle import oracle as orc
         scene = orc.Scene(rgb, K, R, t)
         m = min(a.cpu_sample * 48 // V, n)     # ~10 s of single-core work
         t0 = time.perf_counter()
-        oxy, omask, ocount, _ = scene.score_batch(c_np[:m], ref_np[:m], a.thr, a.wid, nthreads=1)
+        oxy, omask, ocount, _ = scene.score_batch(sw["c_np"][:m], sw["ref_np"][:m], a.thr, a.wid, nthreads=1)
         cdt = time.perf_counter() - t0
-        # the same sample on every host core (OpenMP), SURVEY 8(d) "CPU timing beside it"
         ncores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 10**6))
         t0 = time.perf_counter()
-        scene.score_batch(c_np[:m], ref_np[:m], a.thr, a.wid, nthreads=ncores)
+        scene.score_batch(sw["c_np"][:m], sw["ref_np"][:m], a.thr, a.wid, nthreads=ncores)
         cdt_all = time.perf_counter() - t0
-        # the sample doubles as a parity spot check of the measured launch
-        step(a.wid)
+        # the sample doubles as a parity spot check of the measured kernel
+        ctx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], a.thr, a.wid,
+                         stream=stream.cuda_stream)
         torch.cuda.synchronize()
-        cnt_gpu = count[:m].cpu().numpy()
-        cpu = {"value": m / cdt, "unit": "candidates/s", "cores": 1, "kind": "port",
-               "sample": f"first {m} of the rank-0 sweep (same candidates, wid={a.wid}), "
-                         f"oracle/mvs_oracle.c or_score_batch single-threaded, {cdt:.1f} s",
-               "value_all_cores": m / cdt_all, "cores_all": ncores,
-               "parity_on_sample": bool(np.array_equal(cnt_gpu, ocount) and
-                                        np.array_equal(mask[:m].cpu().numpy().view(np.uint64), omask))}
-        if not cpu["parity_on_sample"]:
+        cnt_gpu = sw["count"][:m].cpu().numpy()
+        out["cpu_baseline"] = {
+            "value": m / cdt, "unit": "candidates/s", "cores": 1, "kind": "port",
+            "sample": f"first {m} of the rank-0 sweep (same candidates, wid={a.wid}), "
+                      f"oracle/mvs_oracle.c or_score_batch single-threaded, {cdt:.1f} s",
+            "value_all_cores": m / cdt_all, "cores_all": ncores,
+            "parity_on_sample": bool(np.array_equal(cnt_gpu, ocount) and
+                                     np.array_equal(sw["mask"][:m].cpu().numpy().view(np.uint64), omask))}
+        if not out["cpu_baseline"]["parity_on_sample"]:
             print("WARNING: GPU/oracle mismatch on the cpu-baseline sample", file=sys.stderr)
-
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            if tj.get("n") == n and tj.get("wid") == a.wid and tj.get("V") == V:
-                traffic = tj.get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    else:
+        out["cpu_baseline"] = None
 
     if rank == 0:
-        out = {
-            "metric": ("candidate patches/sec NCC-scored (640×480, 48 views) at 1/2/4/8 MI355X; % HBM roofline"
-                       if a.scene == "dino" else
-                       "candidate patches/sec NCC-scored (1920×1080, 256 views, synthetic) at 1/2/4/8 MI355X; % HBM roofline"),
-            "value": value,
-            "unit": "candidates/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": dt / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": ("real dinoRing images (data/dinoRing)" if a.scene == "dino" else
-                     "synthetic uniform-random textures (seed 0)") +
-                    " + synthetic candidate patches (seed = rank)",
-            "config": {"workload": f"{'dinoRing' if a.scene == 'dino' else 'ring'} {V}x{W}x{H}, "
-                                   f"one expansion sweep of {n} candidates per GPU, "
-                                   f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
-                                   f"MIN_NCC {a.thr}, accepted set all-gathered",
-                       "global_batch": n * world, "wid": a.wid, "views": V,
-                       "parallelism": f"candidate-queue shards x{world} (RCCL all-gather)"},
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
-                         "unit": "GB/s", "frac": achieved / PEAK_HBM,
-                         "traffic": traffic,
-                         "kernel": ("k_score_tiled5" if V <= 64 and a.kernel != "direct" else
-                                    KERNEL_NAME[a.kernel] if V <= 64 else
-                                    "k_score" if a.kernel == "direct" or V % 4 or V > 256 else
-                                    "k_score_tiledg"),
-                         "kernel_ms": kms, "score_call_ms": pms,
-                         "bytes_per_candidate": B, "candidates_per_launch": n,
-                         # measured DRAM bytes (PMC, profiles/pmc_traffic.json) over
-                         # this run's launch time: the HBM bandwidth really drawn
-                         "traffic_GBps": traffic / (kms * 1e-3) / 1e9 if traffic else None,
-                         "traffic_frac": traffic / (kms * 1e-3) / PEAK_HBM if traffic else None,
-                         "note": "achieved counts every candidate's V windows as if read from "
-                                 "HBM; a tile's candidates share them through LDS, so frac can "
-                                 "exceed 1 while traffic_frac is the HBM share actually used; "
-                                 "the kernel is bound by instruction issue/latency, not HBM or "
-                                 "the LDS pipe (DESIGN.md section 6)"},
-            "cpu_baseline": cpu,
-            "accepted_per_sweep": accepted,
-            "gathered_records": gathered["n"],
-            "secondary": sec,
-        }
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -54,6 +54,11 @@ void mvs_ctx_destroy(mvs_ctx* ctx);
 const char* mvs_last_error(const mvs_ctx* ctx);
 /* Copies the rotations the projection uses (V*9) -- for parity tests. */
 int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp);
+/* The device part of the scene setup again, from the resident RGB images:
+ * the gray stack and its signed view-major copy (k_build_scene).  For
+ * measuring a cold sweep (setup + scoring); stream-ordered (NULL = the
+ * context's stream). */
+int mvs_ctx_rebuild(mvs_ctx* ctx, void* stream);
 
 /* Batched MyPatch.photo_consistenecy_test (MVS2.py:62-77): for candidate i
  * with centre c[3i..3i+2] and reference view ref[i], project into ref[i]
@@ -85,10 +90,11 @@ int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* 
 int mvs_kernel_timing(mvs_ctx* ctx, int enable);
 int mvs_kernel_time(mvs_ctx* ctx, double* total_ms, int64_t* launches);
 const char* mvs_timed_kernel(const mvs_ctx* ctx);
-/* Number of per-view NCC decisions that fell inside the guard band around the
- * threshold (relative 1e-8 on the squared comparison; 1e-9 absolute when
- * min_ncc < 0.01) and were re-evaluated in numpy order since the context was
- * created. */
+/* Number of per-view NCC decisions that fell inside the direct scorer's guard
+ * band around the threshold (relative 1e-8 on the squared comparison; 1e-9
+ * absolute when min_ncc < 0.01) and were re-evaluated in numpy order since the
+ * context was created.  (The tiled scorer's own band, 2e-6 relative on its
+ * binary32 comparison, sends a candidate to the direct scorer.) */
 int64_t mvs_exact_hits(mvs_ctx* ctx);
 
 /* ctNcc (MVS2.py:39-43) on n explicit window pairs of npx (<= 128) uint8
@@ -116,6 +122,10 @@ int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows);
  * queue entries left, candidates scored on the GPU, sweeps, seed candidates,
  * exact-path decisions. */
 int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats);
+/* Host wall seconds per stage phase: times[0] seeding, [1] ordered commit and
+ * sweep planning, [2] GPU sweeps, [3] sweep copy-back, [4] output ordering,
+ * [5] the whole call. */
+int mvs_stage_times(const mvs_stage_result* res, double* times);
 void mvs_stage_free(mvs_stage_result* res);
 
 /* The same stage in steps, for several GPUs (one process and one context per

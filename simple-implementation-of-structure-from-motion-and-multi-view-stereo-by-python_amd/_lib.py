@@ -28,6 +28,7 @@ SIGNATURES = [
                                       _dp, _dp, _dp, _dp, ctypes.POINTER(_vp)]),
     ("mvs_ctx_destroy", None, [_vp]),
     ("mvs_ctx_rproj", ctypes.c_int, [_vp, _dp]),
+    ("mvs_ctx_rebuild", ctypes.c_int, [_vp, _vp]),
     ("mvs_score", ctypes.c_int, [_vp, ctypes.c_int64, _dp, _i32p, ctypes.c_int, ctypes.c_double,
                                  _dp, _u64p, _i32p, _dp]),
     ("mvs_score_device", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int,
@@ -54,6 +55,7 @@ SIGNATURES = [
     ("mvs_stage_count", ctypes.c_int64, [_vp, ctypes.c_int]),
     ("mvs_stage_rows", ctypes.c_int, [_vp, ctypes.c_int, _dp]),
     ("mvs_stage_stats", ctypes.c_int, [_vp, _i64p]),
+    ("mvs_stage_times", ctypes.c_int, [_vp, _dp]),
     ("mvs_stage_free", None, [_vp]),
     ("mvs_expand_candidates", ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, ctypes.c_int64,
                                              _i32p, _i32p, _i32p, ctypes.c_int, ctypes.c_double,
@@ -208,6 +210,11 @@ class MvsContext:
     def exact_hits(self):
         return int(load().mvs_exact_hits(self._h))
 
+    def rebuild(self, stream=None):
+        """Rebuild the device gray stack / view-major copy from the resident
+        RGB images (stream-ordered; for cold-sweep timing)."""
+        check(load().mvs_ctx_rebuild(self._h, stream), self._h, "mvs_ctx_rebuild")
+
     def kernel_timing(self, enable=True):
         """Start (reset) or stop HIP-event timing of the dominant scoring kernel."""
         check(load().mvs_kernel_timing(self._h, 1 if enable else 0), self._h, "mvs_kernel_timing")
@@ -322,6 +329,7 @@ class MvsContext:
 
 STAGE_STATS = ["pops", "tests", "accepts", "queue_left", "scored", "sweeps", "seed_candidates",
                "exact_hits"]
+STAGE_TIMES = ["seed_s", "commit_s", "gpu_sweeps_s", "copy_back_s", "output_s", "total_s"]
 
 
 def _tracks(track_off, obs_view, obs_xy):
@@ -342,9 +350,13 @@ def _take_result(res, h):
             out.append(rows)
         st = np.empty(8, np.int64)
         check(lib.mvs_stage_stats(res, _p(st, _i64p)), h, "mvs_stage_stats")
+        tm = np.empty(6)
+        check(lib.mvs_stage_times(res, _p(tm, _dp)), h, "mvs_stage_times")
     finally:
         lib.mvs_stage_free(res)
-    return out[0], out[1], dict(zip(STAGE_STATS, (int(x) for x in st)))
+    stats = dict(zip(STAGE_STATS, (int(x) for x in st)))
+    stats["times"] = dict(zip(STAGE_TIMES, (float(x) for x in tm)))
+    return out[0], out[1], stats
 
 
 class Stage:

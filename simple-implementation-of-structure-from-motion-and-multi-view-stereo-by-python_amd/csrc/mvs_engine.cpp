@@ -360,6 +360,7 @@ struct mvs_stage_result {
     std::vector<uint8_t> color;     // nrec * 4
     std::vector<int32_t> initial, all;   // record per output row
     int64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double times[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // mvs_stage_times
 };
 
 namespace {
@@ -1112,6 +1113,16 @@ int mvs_kernel_time(mvs_ctx* ctx, double* total_ms, int64_t* launches) {
 
 const char* mvs_timed_kernel(const mvs_ctx* ctx) { return ctx ? ctx->timed_name : ""; }
 
+int mvs_ctx_rebuild(mvs_ctx* ctx, void* stream) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    return guarded(ctx, [&]() {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        if (mvs_launch_build_scene(&ctx->sc, ctx->d_rgb.p, ctx->d_stack.p, ctx->d_gv.p, s) != 0)
+            throw Fail{MVS_E_HIP, "build_scene launch failed"};
+        return 0;
+    });
+}
+
 int mvs_ctx_rproj(const mvs_ctx* ctx, double* Rp) {
     if (!ctx || !Rp) return MVS_E_ARG;
     for (int v = 0; v < ctx->V; ++v) std::memcpy(Rp + 9 * v, ctx->cams[v].Rp, 9 * sizeof(double));
@@ -1194,6 +1205,12 @@ int mvs_stage_run(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off, cons
         const double t2 = Engine::now();
         finish_engine(ctx, E.get(), res.get());
         const double t3 = Engine::now();
+        res->times[0] = t1 - t0;
+        res->times[1] = E->t_plan;
+        res->times[2] = E->t_score;
+        res->times[3] = E->t_fetch;
+        res->times[4] = t3 - t2;
+        res->times[5] = t3 - t0;
         if (std::getenv("MVS_STAGE_TIMES"))
             std::fprintf(stderr, "stage times: seed %.4f s, expand %.4f s (commit/plan %.4f, GPU sweeps %.4f, "
                                  "fetch %.4f), output %.4f s\n",
@@ -1343,6 +1360,12 @@ int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows) {
 int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats) {
     if (!res || !stats) return MVS_E_ARG;
     std::memcpy(stats, res->stats, sizeof res->stats);
+    return 0;
+}
+
+int mvs_stage_times(const mvs_stage_result* res, double* times) {
+    if (!res || !times) return MVS_E_ARG;
+    std::memcpy(times, res->times, 6 * sizeof(double));
     return 0;
 }
 

@@ -150,6 +150,47 @@ def exchange_accepted(count, mask, vlb, group=None):
     return [flat[r * L: r * L + 1 + nbw + sizes[r] * words] for r in range(world)]
 
 
+def exchange_accepted_points(offset, count, mask, c, vlb, group=None):
+    """The sweep's exchange step: every rank's accepted
+    candidates (|V| >= vlb, MVS2.py:256/369) as int64 records
+    [global index, count, mask words..., x, y, z (float64 bits)] -- the 3D
+    points included -- all-gathered over the group (RCCL over xGMI for the
+    nccl backend) with one host synchronisation (the record counts travel
+    first).  offset = global index of this rank's candidate 0.
+    Returns the records of all ranks, concatenated in rank order."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    words = mask.shape[1]
+    width = 2 + words + 3
+    acc = count >= vlb
+    k = acc.sum().to(torch.int64).reshape(1)
+    if world > 1:
+        ks = torch.empty(world, dtype=torch.int64, device=count.device)
+        dist.all_gather_into_tensor(ks, k, group=group)
+    else:
+        ks = k
+    sizes = ks.tolist()                               # the one host sync
+    rank = dist.get_rank(group) if world > 1 else 0
+    kmax = max(max(sizes), 1)
+    buf = torch.zeros((kmax, width), dtype=torch.int64, device=count.device)
+    if sizes[rank]:
+        idx = torch.nonzero_static(acc, size=sizes[rank]).squeeze(1)
+        buf[:sizes[rank], 0] = idx + offset
+        buf[:sizes[rank], 1] = count[idx].to(torch.int64)
+        buf[:sizes[rank], 2:2 + words] = mask[idx].view(torch.int64)
+        buf[:sizes[rank], 2 + words:] = c[idx].contiguous().view(torch.int64)
+    if world == 1:
+        return buf[:sizes[0]]
+    flat = torch.empty((world * kmax, width), dtype=torch.int64, device=count.device)
+    dist.all_gather_into_tensor(flat, buf, group=group)
+    return torch.cat([flat[r * kmax: r * kmax + sizes[r]] for r in range(world)])
+
+
+def unpack_points(rec, words):
+    """-> (global index, count, mask (k, words) int64 view, points (k, 3) float64)."""
+    return rec[:, 0], rec[:, 1].to(torch.int32), rec[:, 2:2 + words], \
+        rec[:, 2 + words:].contiguous().view(torch.float64)
+
+
 _POP8 = None
 
 

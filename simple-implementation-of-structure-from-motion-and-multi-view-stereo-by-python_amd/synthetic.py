@@ -8,6 +8,9 @@ ring_scene(): config 4 -- V views of uniform-random RGB textures on a ring of
 sphere_scene(): a geometrically consistent scene for stage tests -- a
   procedurally textured sphere at the origin rendered into ring cameras
   (black background), plus 2-view seed tracks on its surface.
+sphere_scene_device(): the same kind of scene at config-4 size (256 views of
+  1920x1080), rendered on the GPU with torch (test/bench data generation only),
+  so that sweeps over it accept candidates.
 """
 import numpy as np
 
@@ -111,3 +114,39 @@ def sphere_scene(V=24, H=96, W=128, seed=0, rad=0.02, n_seeds=300, camera_radius
             break
     return (rgb, K, R, t, np.array(off, np.int64), np.array(ov, np.int32),
             np.array(oxy, np.float32).reshape(-1, 2))
+
+
+def sphere_scene_device(V=256, H=1080, W=1920, rad=0.03, camera_radius=0.66, seed=0, device="cuda"):
+    """A textured sphere of radius `rad` at the origin seen by V ring cameras
+    (ring_cameras: dinoRing's K scaled to W x H), black background; rendered
+    per view on `device` with torch.  Returns host (rgb (V,H,W,3) uint8, K, R, t).
+    The texture is a sum of six sinusoids of the surface direction with
+    periods of a few hundred pixels at this size, so neighbouring views agree
+    at the same pixel (the photo test compares every view at the reference
+    view's pixel, MVS2.py:68) and sweeps accept candidates."""
+    import torch
+    rng = np.random.default_rng(seed)
+    K, R, t = ring_cameras(V, H, W, camera_radius)
+    freqs = torch.tensor(rng.normal(0, 1, (6, 3)) * 6.0, dtype=torch.float64, device=device)
+    phases = torch.tensor(rng.uniform(0, 2 * np.pi, 6), dtype=torch.float64, device=device)
+    ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64, device=device),
+                            torch.arange(W, dtype=torch.float64, device=device), indexing="ij")
+    pix = torch.stack([xs + 0.5, ys + 0.5, torch.ones_like(xs)], -1)
+    out = np.empty((V, H, W, 3), np.uint8)
+    for v in range(V):
+        Kinv = torch.tensor(np.linalg.inv(K[v]), device=device)
+        Rv = torch.tensor(R[v], device=device)
+        d = pix @ Kinv.T @ Rv
+        d = d / d.norm(dim=-1, keepdim=True)
+        O = torch.tensor(-R[v].T @ t[v], device=device)
+        b = d @ O
+        disc = b * b - (O @ O - rad * rad)
+        hit = disc > 0
+        s = -b - torch.sqrt(torch.clamp(disc, min=0))
+        X = O + s.unsqueeze(-1) * d
+        nrm = X / rad
+        g = 128 + 20 * torch.sin(nrm @ freqs.T + phases).sum(-1)
+        g = torch.where(hit, torch.clamp(g, 0, 255), torch.zeros_like(g))
+        rgb = torch.stack([g, 0.9 * g, 0.8 * g], -1).to(torch.uint8)
+        out[v] = rgb.cpu().numpy()
+    return out, K, R, t

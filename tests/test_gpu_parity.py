@@ -412,6 +412,8 @@ def test_stage_stepped_single_rank_matches_run(pkg, ctx, seeds):
     ini, allp, st = ctx.stage(*args, cell_size=2, scale=10.0, wid=5, max_pops=20000)
     ini2, allp2, st2 = par.stage_sharded(ctx, *args, cell_size=2, scale=10.0, wid=5, max_pops=20000)
     assert np.array_equal(ini, ini2) and np.array_equal(allp, allp2)
+    assert st.pop("times")["total_s"] > 0.0
+    st2.pop("times")
     assert st == st2
 
 
