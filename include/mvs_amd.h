@@ -115,9 +115,13 @@ int mvs_ncc_windows(int64_t n, int npx, const uint8_t* d_a, const uint8_t* d_b, 
 int mvs_stage_run(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off,
                   const int32_t* obs_view, const float* obs_xy, int cell_size, double scale,
                   int wid, int64_t max_pops, mvs_stage_result** out);
-/* which = 0: initial_patches rows, 1: all_patches rows (x,y,z,r,g,b float64). */
+/* which = 0: initial_patches rows, 1: all_patches rows (x,y,z,r,g,b float64).
+ * The rows are ordered and gathered on the device; mvs_stage_rows copies them
+ * into a host buffer, mvs_stage_rows_device into a device buffer
+ * (stream-ordered). */
 int64_t mvs_stage_count(const mvs_stage_result* res, int which);
 int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows);
+int mvs_stage_rows_device(const mvs_stage_result* res, int which, double* d_rows, void* stream);
 /* stats[0..7] = pops, reference-equivalent photo tests, accepted patches,
  * queue entries left, candidates scored on the GPU, sweeps, seed candidates,
  * exact-path decisions. */

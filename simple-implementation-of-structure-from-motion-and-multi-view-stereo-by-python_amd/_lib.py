@@ -54,6 +54,7 @@ SIGNATURES = [
     ("mvs_stage_destroy", None, [_vp]),
     ("mvs_stage_count", ctypes.c_int64, [_vp, ctypes.c_int]),
     ("mvs_stage_rows", ctypes.c_int, [_vp, ctypes.c_int, _dp]),
+    ("mvs_stage_rows_device", ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
     ("mvs_stage_stats", ctypes.c_int, [_vp, _i64p]),
     ("mvs_stage_times", ctypes.c_int, [_vp, _dp]),
     ("mvs_stage_free", None, [_vp]),
@@ -330,6 +331,7 @@ class MvsContext:
 STAGE_STATS = ["pops", "tests", "accepts", "queue_left", "scored", "sweeps", "seed_candidates",
                "exact_hits"]
 STAGE_TIMES = ["seed_s", "commit_s", "gpu_sweeps_s", "copy_back_s", "output_s", "total_s"]
+# + "rows_to_host_s": the copy of the PLY rows from HBM into the numpy arrays
 
 
 def _tracks(track_off, obs_view, obs_xy):
@@ -339,8 +341,10 @@ def _tracks(track_off, obs_view, obs_xy):
 
 def _take_result(res, h):
     """Copy an mvs_stage_result out and free it -> (initial, all, stats)."""
+    import time
     lib = load()
     try:
+        t0 = time.perf_counter()
         out = []
         for which in (0, 1):
             n = lib.mvs_stage_count(res, which)
@@ -348,6 +352,7 @@ def _take_result(res, h):
             if n:
                 check(lib.mvs_stage_rows(res, which, _p(rows, _dp)), h, "mvs_stage_rows")
             out.append(rows)
+        t_rows = time.perf_counter() - t0
         st = np.empty(8, np.int64)
         check(lib.mvs_stage_stats(res, _p(st, _i64p)), h, "mvs_stage_stats")
         tm = np.empty(6)
@@ -356,6 +361,7 @@ def _take_result(res, h):
         lib.mvs_stage_free(res)
     stats = dict(zip(STAGE_STATS, (int(x) for x in st)))
     stats["times"] = dict(zip(STAGE_TIMES, (float(x) for x in tm)))
+    stats["times"]["rows_to_host_s"] = t_rows
     return out[0], out[1], stats
 
 

@@ -352,13 +352,13 @@ struct mvs_ctx {
 };
 
 struct mvs_stage;
-// The stage's outputs as record indices into the records' centres and
-// colours; mvs_stage_rows writes the [x y z r g b] rows straight into the
-// caller's buffer (no intermediate copy of the ~35 MB of rows).
+// The stage's outputs: the [x y z r g b] rows of initial_patches and
+// all_patches, ordered and gathered on the device (HBM); mvs_stage_rows copies
+// them straight into the caller's buffer.
 struct mvs_stage_result {
-    std::vector<double> c;          // nrec * 3
-    std::vector<uint8_t> color;     // nrec * 4
-    std::vector<int32_t> initial, all;   // record per output row
+    int device = 0;
+    DevBuf<double> d_init, d_all;   // rows * 6
+    int64_t n_init = 0, n_all = 0;
     int64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     double times[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // mvs_stage_times
 };
@@ -902,51 +902,68 @@ struct Engine {
     // reconstruct_from_Q order (MVS2.py:159-173): key (view, ci, cj)
     // lexicographic, append order within a key, first sight of each object.  A
     // patch is appended under (u, cell) for every u in its V list, so its first
-    // sight is at (min u, cell), in fill order among equal keys.
-    double t_out[5] = {0, 0, 0, 0, 0};   // copy-back, keys, sort, rows, end stamp (MVS_STAGE_TIMES)
+    // sight is at (min u, cell), in fill order among equal keys: a stable sort
+    // of the acceptance events by (min view, cell x, cell y).  All on the
+    // device: event keys (k_event_keys), a stable LSD radix sort (hipCUB) and
+    // the row gather (k_gather_rows) into the result's HBM rows.
+    double t_out[5] = {0, 0, 0, 0, 0};   // upload, keys + sort, rows, -, end stamp (MVS_STAGE_TIMES)
+    DevBuf<int32_t> o_ev, o_vals, o_init;
+    DevBuf<uint64_t> o_keys, o_keys_s;
+    DevBuf<uint8_t> o_tmp;
 
     void output(mvs_stage_result* res) {
         double ta = now();
-        res->c.resize(nrec * 3);
-        res->color.resize(nrec * 4);
-        if (nrec) {
-            HIPCHK(hipMemcpyAsync(res->c.data(), d_c.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(res->color.data(), d_color.p, nrec * 4, hipMemcpyDeviceToHost, s));
+        const int64_t nev = (int64_t)events.size();
+        res->device = ctx->device;
+        res->n_init = n_seeds;
+        res->d_init.alloc((size_t)std::max<int64_t>(n_seeds, 1) * 6);
+        if (n_seeds) {
+            o_init.ensure(n_seeds);
+            std::vector<int32_t> ids(n_seeds);
+            for (int64_t r = 0; r < n_seeds; ++r) ids[r] = (int32_t)r;
+            HIPCHK(hipMemcpyAsync(o_init.p, ids.data(), n_seeds * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            if (mvs_launch_gather_rows(recs(), o_init.p, n_seeds, res->d_init.p, s) != 0)
+                throw Fail{MVS_E_HIP, "gather_rows launch failed"};
+            HIPCHK(hipStreamSynchronize(s));   // ids leaves scope
+        }
+        res->d_all.alloc((size_t)std::max<int64_t>(nev, 1) * 6);
+        if (nev) {
+            o_ev.ensure(nev);
+            o_vals.ensure(nev);
+            o_keys.ensure(nev);
+            o_keys_s.ensure(nev);
+            HIPCHK(hipMemcpyAsync(o_ev.p, events.data(), nev * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            double tb = now();
+            t_out[0] = tb - ta;
+            if (mvs_launch_event_keys(recs(), words, o_ev.p, nev, nci, ncj, o_keys.p, s) != 0)
+                throw Fail{MVS_E_HIP, "event_keys launch failed"};
+            const uint64_t kmax = (uint64_t)V * nci * ncj;   // keys < kmax; never-emitted events: ~0
+            int bits = 1;
+            while (bits < 63 && (1ull << bits) <= kmax) ++bits;
+            size_t tmp_bytes = 0;
+            if (mvs_sort_pairs(nullptr, &tmp_bytes, o_keys.p, o_keys_s.p, o_ev.p, o_vals.p, nev, bits, s) != 0)
+                throw Fail{MVS_E_HIP, "sort sizing failed"};
+            o_tmp.ensure(tmp_bytes);
+            if (mvs_sort_pairs(o_tmp.p, &tmp_bytes, o_keys.p, o_keys_s.p, o_ev.p, o_vals.p, nev, bits, s) != 0)
+                throw Fail{MVS_E_HIP, "sort failed"};
+            // emitted events = keys below kmax; the never-emitted (~0) sort last
+            uint64_t last = 0;
+            HIPCHK(hipMemcpyAsync(&last, o_keys_s.p + nev - 1, sizeof last, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
+            int64_t n_all = nev;
+            if (last >= kmax) {
+                std::vector<uint64_t> ks(nev);
+                HIPCHK(hipMemcpy(ks.data(), o_keys_s.p, nev * sizeof(uint64_t), hipMemcpyDeviceToHost));
+                n_all = std::lower_bound(ks.begin(), ks.end(), kmax) - ks.begin();
+            }
+            double tc = now();
+            t_out[1] = tc - tb;
+            res->n_all = n_all;
+            if (mvs_launch_gather_rows(recs(), o_vals.p, n_all, res->d_all.p, s) != 0)
+                throw Fail{MVS_E_HIP, "gather_rows launch failed"};
+            HIPCHK(hipStreamSynchronize(s));
+            t_out[2] = now() - tc;
         }
-        double tb = now();
-        t_out[0] = tb - ta;
-        res->initial.resize(n_seeds);
-        for (int64_t r = 0; r < n_seeds; ++r) res->initial[r] = (int32_t)r;
-        // stable sort of the events by key (min view, cell x, cell y): LSD radix
-        // sort, 11 bits per pass (the key space is V * nci * ncj)
-        std::vector<uint64_t> keyed, tmp;   // key << 32 | event index
-        keyed.reserve(events.size());
-        for (size_t e = 0; e < events.size(); ++e) {
-            const int64_t r = events[e];
-            int minv = -1;
-            for (int w = 0; w < words && minv < 0; ++w)
-                if (h_mask[r * words + w]) minv = 64 * w + __builtin_ctzll(h_mask[r * words + w]);
-            const int cx = h_cell[2 * r], cy = h_cell[2 * r + 1];
-            if (minv < 0 || cx < 0 || cx >= nci || cy < 0 || cy >= ncj) continue;
-            keyed.push_back(((uint64_t)(((int64_t)minv * nci + cx) * ncj + cy) << 32) | (uint64_t)e);
-        }
-        const uint64_t kmax = (uint64_t)V * nci * ncj;
-        double tc = now();
-        t_out[1] = tc - tb;
-        tmp.resize(keyed.size());
-        for (int shift = 32; shift < 64 && (kmax >> (shift - 32)) > 0; shift += 11) {
-            size_t cnt[2049] = {0};
-            for (uint64_t k : keyed) ++cnt[((k >> shift) & 2047) + 1];
-            for (int b = 0; b < 2048; ++b) cnt[b + 1] += cnt[b];
-            for (uint64_t k : keyed) tmp[cnt[(k >> shift) & 2047]++] = k;
-            keyed.swap(tmp);
-        }
-        double td = now();
-        t_out[2] = td - tc;
-        res->all.resize(keyed.size());
-        for (size_t i = 0; i < keyed.size(); ++i) res->all[i] = events[(uint32_t)keyed[i]];
-        t_out[3] = now() - td;
         res->stats[0] = stat_pops;
         res->stats[1] = stat_tests;
         res->stats[2] = (int64_t)events.size();
@@ -1216,8 +1233,8 @@ int mvs_stage_run(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off, cons
                                  "fetch %.4f), output %.4f s\n",
                          t1 - t0, t2 - t1, E->t_plan, E->t_score, E->t_fetch, t3 - t2);
         if (std::getenv("MVS_STAGE_TIMES"))
-            std::fprintf(stderr, "  output: copy-back %.4f, keys %.4f, sort %.4f, rows %.4f s; output() %.4f s\n",
-                         E->t_out[0], E->t_out[1], E->t_out[2], E->t_out[3], E->t_out[4]);
+            std::fprintf(stderr, "  output: events upload %.4f, keys + sort %.4f, row gather %.4f s; output() %.4f s\n",
+                         E->t_out[0], E->t_out[1], E->t_out[2], E->t_out[4]);
         *out = res.release();
         if (std::getenv("MVS_STAGE_TIMES")) {
             const double td = Engine::now();
@@ -1336,24 +1353,28 @@ void mvs_stage_destroy(mvs_stage* st) {
 
 int64_t mvs_stage_count(const mvs_stage_result* res, int which) {
     if (!res) return MVS_E_ARG;
-    return (int64_t)(which ? res->all.size() : res->initial.size());
+    return which ? res->n_all : res->n_init;
 }
 
 int mvs_stage_rows(const mvs_stage_result* res, int which, double* rows) {
     if (!res || !rows) return MVS_E_ARG;
-    const std::vector<int32_t>& idx = which ? res->all : res->initial;
-    const double* c = res->c.data();
-    const uint8_t* col = res->color.data();
-    for (size_t i = 0; i < idx.size(); ++i) {
-        const int64_t r = idx[i];
-        double* o = rows + 6 * i;
-        o[0] = c[3 * r];
-        o[1] = c[3 * r + 1];
-        o[2] = c[3 * r + 2];
-        o[3] = col[4 * r];
-        o[4] = col[4 * r + 1];
-        o[5] = col[4 * r + 2];
-    }
+    const int64_t n = which ? res->n_all : res->n_init;
+    if (n == 0) return 0;
+    if (hipSetDevice(res->device) != hipSuccess ||
+        hipMemcpy(rows, which ? res->d_all.p : res->d_init.p, n * 6 * sizeof(double), hipMemcpyDeviceToHost) !=
+            hipSuccess)
+        return set_err(nullptr, Fail{MVS_E_HIP, "rows copy failed"});
+    return 0;
+}
+
+int mvs_stage_rows_device(const mvs_stage_result* res, int which, double* d_rows, void* stream) {
+    if (!res || !d_rows) return MVS_E_ARG;
+    const int64_t n = which ? res->n_all : res->n_init;
+    if (n == 0) return 0;
+    if (hipSetDevice(res->device) != hipSuccess ||
+        hipMemcpyAsync(d_rows, which ? res->d_all.p : res->d_init.p, n * 6 * sizeof(double),
+                       hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess)
+        return set_err(nullptr, Fail{MVS_E_HIP, "rows copy failed"});
     return 0;
 }
 
@@ -1369,7 +1390,11 @@ int mvs_stage_times(const mvs_stage_result* res, double* times) {
     return 0;
 }
 
-void mvs_stage_free(mvs_stage_result* res) { delete res; }
+void mvs_stage_free(mvs_stage_result* res) {
+    if (!res) return;
+    (void)hipSetDevice(res->device);
+    delete res;
+}
 
 int mvs_expand_candidates(mvs_ctx* ctx, int64_t n_parents, const double* pc, const double* pn,
                           const double* pxy, int64_t n_jobs, const int32_t* job_parent,

@@ -212,3 +212,62 @@ def test_compact_exchange_gloo(tmp_path, world, n, words):
         assert np.array_equal(z["idx"], exp_i)
         assert np.array_equal(z["count"], exp_c)
         assert np.array_equal(z["mask"], exp_m)
+
+
+def _points_worker(rank, world, port, n, strong, out_dir):
+    import importlib
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, GOLDEN)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    par = importlib.import_module(PKG_NAME + ".parallel")
+    syn = importlib.import_module(PKG_NAME + ".synthetic")
+    from make_seeds import load_dino
+    from oracle import oracle as orc
+    imgs, K, R, t = load_dino(DATA)
+    sc = orc.Scene(np.stack(imgs), K, R, t)
+    if strong:      # one queue of n candidates, rank r scores its shard_range slice
+        c, ref = syn.candidates(n, K, R, t, seed=17)
+        b, e = par.shard_range(n, rank, world)
+        c, ref, off = c[b:e], ref[b:e], b
+    else:           # weak: block r of a queue of world * n candidates
+        c, ref = syn.candidates(n, K, R, t, seed=17 + rank)
+        off = rank * n
+    _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
+    rec = par.exchange_accepted_points(off, torch.from_numpy(count), torch.from_numpy(mask.view(np.int64)),
+                                       torch.from_numpy(np.ascontiguousarray(c)), 3)
+    idx, cnt, m, pts = par.unpack_points(rec, 1)
+    np.savez(os.path.join(out_dir, f"p{rank}.npz"), idx=idx.numpy(), count=cnt.numpy(), mask=m.numpy(),
+             pts=pts.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,strong", [(2, 500, False), (3, 401, True)])
+def test_accepted_points_exchange_gloo(tmp_path, orc, dino, world, n, strong):
+    """The bench's sweep exchange (bench.py, parallel.exchange_accepted_points):
+    the candidate queue split over the ranks -- per-rank blocks (weak) or
+    shard_range slices of one queue (strong) -- and every rank ends with the
+    whole sweep's accepted records, 3D points included, as one process
+    scoring the whole queue would produce them."""
+    import importlib
+    syn = importlib.import_module(PKG_NAME + ".synthetic")
+    mp.spawn(_points_worker, args=(world, _free_port(), n, strong, str(tmp_path)), nprocs=world, join=True)
+    rgb, K, R, t = dino
+    sc = orc.Scene(rgb, K, R, t)
+    if strong:
+        c, ref = syn.candidates(n, K, R, t, seed=17)
+    else:
+        parts = [syn.candidates(n, K, R, t, seed=17 + r) for r in range(world)]
+        c = np.concatenate([p[0] for p in parts])
+        ref = np.concatenate([p[1] for p in parts])
+    _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
+    exp = np.nonzero(count >= 3)[0]
+    assert len(exp) > 0
+    for r in range(world):
+        z = np.load(tmp_path / f"p{r}.npz")
+        assert np.array_equal(z["idx"], exp)
+        assert np.array_equal(z["count"], count[exp])
+        assert np.array_equal(z["mask"].view(np.uint64), mask[exp])
+        assert np.array_equal(z["pts"], c[exp])
