@@ -918,7 +918,8 @@ __device__ unsigned long long g_stamps[4096 * 8];
 #endif
 
 struct alignas(16) CandInfo {
-    int32_t px, R, Sa, idx;   // pixel in the tile, reference view (-1: no candidate), -S_a, batch index
+    int32_t px, R, Sa, idx;   // table row of its pixel (px * views per row), reference view (-1: no
+                              // candidate), -S_a, batch index
     float T, gT;              // decision threshold on num w_b and its guard band
     double ca;                // n / (n-1) * w_a
 };
@@ -1041,7 +1042,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     if (tid < 8) ((uint32_t*)(smem + L.zero))[tid] = 0u;
 
     const double kn = (double)NPX / (double)(NPX - 1);
-    const double tq = a.thr / kn;
+    const float tqf = (float)(a.thr / kn);
     const int n_units = t.item_off[t.ntiles];
     int32_t* head = &t.tile_count[t.ntiles];
     const int m = lane & 15, kh = lane >> 4;
@@ -1188,9 +1189,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                     const int db = NPX * q - sg * sg;   // < 2^31: n * sum g^2 <= 121 * 121 * 255^2
                     double w = __builtin_nan("");       // constant window: ctNcc's nan
                     if (db > 0) {
+                        // v_rsq_f64 + one Newton step: max relative error 4.1e-15 over
+                        // 4M values of D < 2^31 (tools/ubench/rsq_acc.hip; 5.2e-8 without)
                         const double D = (double)db;
                         w = __builtin_amdgcn_rsq(D);
-                        w = w * (1.5 - 0.5 * D * w * w);
                         w = w * (1.5 - 0.5 * D * w * w);
                     }
                     ms[y] = sg - 128 * NPX;             // S_b of s = g - 128
@@ -1275,13 +1277,14 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 double my_ca = 0.0;
                 if (kh == 0) {
                     CandInfo c;
-                    c.px = e.y & 127;                    // rrel * 16 + qrel
-                    const int o = c.px * VP + R;
+                    c.px = (e.y & 127) * VP;             // (rrel * 16 + qrel) * VP
+                    const int o = c.px + R;
                     const double wa = tw[o];
                     c.R = valid ? R : -1;
                     c.Sa = -tsb[o];                      // -S_a: num = n C + (-S_a) S_b
                     c.idx = e.x;
-                    c.T = valid ? (float)(tq / wa) : __builtin_nanf("");
+                    // T = thr (n-1)/n sqrt(da) in binary32 (1-ulp reciprocal, well inside the guard band)
+                    c.T = valid ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf("");
                     c.gT = 2e-6f * fabsf(c.T);
                     c.ca = kn * wa;
                     ci[m] = c;
@@ -1300,7 +1303,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                     static_for<NBLK>([&](auto Nc) {
                         constexpr int nb = Nc;
                         const int vl = 16 * nb + m;
-                        const int o = c.px * VP + vl;
+                        const int o = c.px + vl;
                         const int num = __mul24(c.Sa, tsb[o]) + __mul24(NPX, C[nb][i]);
                         const double w = tw[o];
                         // lane masks straight from v_cmp (a ballot of a bool would

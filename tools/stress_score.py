@@ -1,5 +1,5 @@
 """Randomised parity sweep of the photo-test scorers (auto kernel choice:
-k_score_tiled3 / k_score_tiledg / k_score / v1 tiled) against the oracle over
+(k_score_mma, its view-group path for V > 64, and the direct k_score) against the oracle over
 view counts, image sizes (incl. widths not a multiple of 4), window sizes and
 thresholds.  Prints every mismatch; exit 1 if any."""
 import importlib, itertools, sys
