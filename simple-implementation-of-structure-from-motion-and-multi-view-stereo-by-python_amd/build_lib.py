@@ -40,8 +40,23 @@ def build(force=False, verbose=False, stamps=False):
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd, cwd=CSRC)
+    check_undefined(out + ".tmp")
     os.replace(out + ".tmp", out)
     return out
+
+
+def check_undefined(path):
+    """A kernel template whose body the host pass rejects without a
+    diagnostic leaves its launch stub undefined: the .so links, then fails to
+    load.  Refuse such a build here."""
+    nm = "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not os.path.exists(nm):
+        return
+    undef = subprocess.run([nm, "--undefined-only", path], capture_output=True, text=True, check=True).stdout
+    bad = [ln.split()[-1] for ln in undef.splitlines() if "_GLOBAL__N_" in ln]
+    if bad:
+        os.remove(path)
+        raise RuntimeError(f"{len(bad)} kernel(s) of this build have no host stub, e.g. {bad[0]}")
 
 
 if __name__ == "__main__":

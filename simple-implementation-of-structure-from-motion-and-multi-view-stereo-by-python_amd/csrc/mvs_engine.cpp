@@ -305,9 +305,8 @@ struct mvs_ctx {
     DevBuf<int32_t> s_ref, s_count;
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
-    DevBuf<int32_t> t_tiles, t_cand, t_pcnt;
+    DevBuf<int32_t> t_tiles, t_cand;
     DevBuf<int4> t_items;
-    DevBuf<double> t_psum;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
     DevBuf<float> f_resp, f_dil;
     DevBuf<uint32_t> f_key, f_desc;
@@ -441,16 +440,11 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         ctx->t_tiles.ensure((size_t)3 * (ntiles + 2) + 8);
         if (ctx->t_tiles.p != tiles_before) ctx->tiles_clean_ntiles = -1;
         const int groups = grouped ? (ctx->V + MVS_GROUP_VIEWS - 1) / MVS_GROUP_VIEWS : 1;
-        ctx->t_cand.ensure((size_t)(5 + groups) * n);   // fix_list: one entry per (candidate, group)
+        ctx->t_cand.ensure((size_t)6 * n);
         t.ntiles = ntiles;
         t.chunk = grouped ? MVS_GROUP_CHUNK : MVS_MMA_CHUNK;
         t.groups = groups;
-        if (grouped) {
-            ctx->t_pcnt.ensure((size_t)groups * n);
-            ctx->t_psum.ensure((size_t)groups * n);
-            t.part_cnt = ctx->t_pcnt.p;
-            t.part_sum = ctx->t_psum.p;
-        }
+        t.tile_major = grouped ? 1 : 0;   // k_score_mma_v: neighbouring tiles in flight together
         t.tile_count = ctx->t_tiles.p;
         t.tile_off = ctx->t_tiles.p + (ntiles + 2);
         t.item_off = ctx->t_tiles.p + 2 * (ntiles + 2);

@@ -60,7 +60,7 @@ struct ScoreArgs {
 //   cand_key[n]  = tile (or -1 if the window is invalid), cand_rank[n],
 //   cand_pk[n]   = (x - x0) | (y - y0) << 4 | R << 7 (pixel inside the tile),
 //   sorted[n]    = {id, pk} grouped by tile
-//   fix_list[n*groups], fix_count[1]: candidates with a view decision inside
+//   fix_list[n], fix_count[1]: candidates with a view decision inside
 //   the guard band, re-scored by k_score_fix (numpy-order ctNcc) afterwards
 struct TiledArgs {
     int ntx, nty, ntiles;
@@ -75,12 +75,9 @@ struct TiledArgs {
     int2* sorted;
     int32_t* fix_list;
     int32_t* fix_count;
-    // view groups (V > 64): work unit = (work item, group of 64 views); per
-    // (candidate, group) partial count and sum of passing ncc, reduced by
-    // k_group_finalize.  groups = 1 otherwise.
+    // view groups of 64 (V > 64: k_score_mma_v scores each work item against
+    // every group in turn); groups = 1 otherwise
     int groups;
-    int32_t* part_cnt;         // n*groups
-    double* part_sum;          // n*groups
     // k_tile_scan leaves every counter zero for the next batch (it zeroes the
     // bin counts after reading them and the queue head / fix_count before the
     // scorer uses them); zero_first = 1 asks the launcher to clear them first
@@ -88,9 +85,10 @@ struct TiledArgs {
     int zero_first;
     // work items in the order the scorer takes them (k_tile_scan): every full
     // chunk first, then the partial (last) chunks by decreasing size, so the
-    // dynamic queue ends on the shortest items; int4 = (tile, first sorted
-    // candidate, candidates, 0)
+    // dynamic queue ends on the shortest items; or, tile_major = 1, in tile
+    // order; int4 = (tile, first sorted candidate, candidates, 0)
     int4* items;
+    int tile_major;
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).
@@ -129,7 +127,7 @@ struct ExpandArgs {
 #define MVS_TILE_H 8
 #define MVS_MMA_CHUNK 1024    // candidates per work item, V <= 64 (whole tiles, as a rule)
 #define MVS_GROUP_VIEWS 64    // views per group when V > 64
-#define MVS_GROUP_CHUNK 64    // candidates per work item when V > 64
+#define MVS_GROUP_CHUNK 116   // candidates per work item when V > 64 (their reference rows staged)
 
 extern "C" {
 // RGB -> stack and gv (one pass, coalesced on both sides); the caller zeroes
@@ -140,8 +138,8 @@ int mvs_launch_build_scene(const SceneDev* sc, const uint8_t* d_rgb, uint8_t* d_
 // on s immediately before and after the kernel
 int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s,
                      hipEvent_t ev0, hipEvent_t ev1);
-// tiled scorer: k_bin, k_tile_scan, k_scatter, k_score_mma (timed by ev0/ev1),
-// [k_group_finalize,] k_score_fix
+// tiled scorer: k_bin, k_tile_scan, k_scatter, k_score_mma or k_score_mma_v
+// (timed by ev0/ev1), k_score_fix
 int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
                            hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 // dynamic LDS bytes of k_score_mma (0 if the configuration is unsupported)

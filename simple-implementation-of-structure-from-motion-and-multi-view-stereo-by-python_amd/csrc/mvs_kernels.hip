@@ -424,10 +424,11 @@ DEV void block_scan_1024(int32_t (&v)[N], int32_t* wtot /* LDS, 16 * N */) {
 }
 
 // Exclusive scans of tile counts and work items (one workgroup), and the
-// work-item list in longest-first order: all full chunks (tile-major), then
-// the partial chunks by decreasing candidate count.  A dynamic queue handed
+// work-item list, either longest-first: all full chunks (tile-major), then
+// the partial chunks by decreasing candidate count (a dynamic queue handed
 // out in that order ends on its shortest items, which trims the tail where a
-// few workgroups still run while the rest of the chip idles.
+// few workgroups still run while the rest of the chip idles), or tile-major
+// (t.tile_major: neighbouring tiles in flight together).
 __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
     __shared__ int32_t wtot[16 * 3];
     __shared__ int32_t tot[3];
@@ -471,9 +472,16 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
         rc += c;
         ri += (c + t.chunk - 1) / t.chunk;
         const int full = c / t.chunk, rem = c - full * t.chunk;
-        for (int j = 0; j < full; ++j) t.items[rf + j] = make_int4(k, rc - c + j * t.chunk, t.chunk, 0);
+        if (t.tile_major) {
+            // the tile's chunks at its own item offset
+            for (int j = 0; j < full + (rem ? 1 : 0); ++j)
+                t.items[ri - (c + t.chunk - 1) / t.chunk + j] =
+                    make_int4(k, rc - c + j * t.chunk, j < full ? t.chunk : rem, 0);
+        } else {
+            for (int j = 0; j < full; ++j) t.items[rf + j] = make_int4(k, rc - c + j * t.chunk, t.chunk, 0);
+            if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int4(k, rc - c + full * t.chunk, rem, 0);
+        }
         rf += full;
-        if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int4(k, rc - c + full * t.chunk, rem, 0);
         t.tile_count[k] = 0;          // clean for the next batch's k_bin
     }
     if (tid == 1023) {
@@ -496,27 +504,12 @@ __global__ void k_scatter(const ScoreArgs a, const TiledArgs t) {
 }
 
 // ---------------------------------------------------------------------------
-// Tiled scorer, stage 2: k_score_mma.  A workgroup (16 waves) takes one work
-// item (the candidates of one 16x8 pixel tile, or a 64-candidate chunk of it
-// per group of 64 views when V > 64) from a dynamic queue and
-//   1. stages the tile's window region of every view in LDS as signed bytes
-//      s = g - 128, [view][18 rows][32 columns] (two aligned 16-B loads of the
-//      view-major gray copy per view row);
-//   2. computes the window moments S_b = sum s and n S_bb - S_b^2 of every view
-//      at every pixel of the tile from the staged region (horizontal window
-//      sums by v_dot4_i32_i8 prefixes, then vertical sums);
-//   3. scores the candidates 16 at a time per wave on the matrix cores:
-//      C[m][v] = sum_k A[m][k] B[k][v] with k = the 18x32 region pixels,
-//      A[m][k] = s_{R_m}(k) masked to candidate m's window, B[k][v] = s_v(k):
-//      v_mfma_i32_16x16x64_i8 over 9 K-steps of two region rows, one 16-view
-//      block per MFMA; C = sum over the window of s_R s_v, exact;
-//   4. decides every (candidate, view) pair from the exact integers: with
-//      num = n C - S_a S_b (shift invariant: the n S_ab - S_a S_b of ctNcc),
-//      ncc > thr  <=>  num |num| > sgn(thr) (thr (n-1)/n)^2 da db, evaluated in
-//      binary32 with a relative guard band of 2e-6 (the binary32 roundings add
-//      < 5e-7); a candidate with any pair inside the band is re-scored by
-//      k_score_fix (numpy-order ctNcc).  avg_ncc_score from binary64
-//      num * n/((n-1) sqrt(da)) * rsqrt(db).
+// Tiled scorer, stage 2: the candidates of a 16x8 pixel tile against every
+// view on the matrix cores (v_mfma_i32_16x16x64_i8 over the tile's window
+// region), one workgroup of 16 waves per CU taking work items from a dynamic
+// queue: k_score_mma for V <= 64 (every view staged), k_score_mma_v for V > 64
+// (64-view groups).  Both decide each (candidate, view) pair from exact
+// integer window products and moments (see k_score_mma).
 // ---------------------------------------------------------------------------
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -539,39 +532,8 @@ struct MmaGeom {
     static_assert(ROWS % 2 == 0, "K-steps take two rows");
 };
 
-// per-wave slot of one candidate of the M-block being scored
-struct alignas(16) CandInfoG {
-    int32_t px, R, Sa, da;   // pixel in the tile, reference view, its window moments
-    double ca;               // n / ((n-1) sqrt(da))
-    float tkda;              // (thr (n-1)/n)^2 da
-    int32_t idx;
-};
-
-struct MmaLdsG {
-    int reg, mom, ci, wsum, zero, areg, asum, total;
-};
-
-template <int WID>
-__host__ __device__ inline MmaLdsG mma_lds_g(int VR, int VP, bool grouped) {
-    using G = MmaGeom<WID>;
-    MmaLdsG L;
-    L.reg = 0;
-    L.mom = VR * G::VS;
-    const int htmp = G::ROWS * 16 * VP * 4, mom = 128 * VP * 8;   // aliased: horizontal sums, then the table
-    L.ci = L.mom + (htmp > mom ? htmp : mom);
-    L.wsum = L.ci + kMmaWaves * 16 * (int)sizeof(CandInfoG);
-    L.zero = L.wsum + kMmaWaves * 16 * 8;
-    L.areg = L.zero + 32;
-    L.asum = L.areg + (grouped ? kGroupChunk * G::NB * 32 : 0);
-    L.total = L.asum + (grouped ? kGroupChunk * 8 : 0);
-    return L;
-}
-
 // 4-bit column mask -> byte mask
 DEV uint32_t byte_mask(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xffu; }
-
-// gv holds s = g - 128 already
-DEV uint4 load_signed(const uint8_t* p) { return *(const uint4*)p; }
 
 // 1/k for k = 0..64 (entry 0 unused), correctly rounded at compile time
 struct RecipTable {
@@ -581,302 +543,6 @@ struct RecipTable {
     }
 };
 __constant__ constexpr RecipTable c_recip{};
-
-template <int WID, int NBLK, bool GROUPED>
-__global__ __launch_bounds__(kMmaThreads) void k_score_mma_g(const SceneDev sc, const ScoreArgs a,
-                                                           const TiledArgs t) {
-    using G = MmaGeom<WID>;
-    constexpr int NB = G::NB, NPX = G::NPX, ROWS = G::ROWS, KS = G::KS, VS = G::VS, C0 = G::C0;
-    constexpr int VP = 16 * NBLK;              // views per moments-table row
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_unit;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int V = sc.V;
-    const int NG = GROUPED ? t.groups : 1;
-    const int words = (V + 63) >> 6;
-    const MmaLdsG L = mma_lds_g<WID>(GROUPED ? kGroupViews : V, VP, GROUPED);
-    uint8_t* reg = smem + L.reg;
-    uint32_t* htmp = (uint32_t*)(smem + L.mom);
-    int2* mom = (int2*)(smem + L.mom);
-    CandInfoG* ci = (CandInfoG*)(smem + L.ci) + wave * 16;
-    double* wsum = (double*)(smem + L.wsum) + wave * 16;
-    uint8_t* areg = smem + L.areg;
-    int2* asum = (int2*)(smem + L.asum);
-    if (tid < 8) ((uint32_t*)(smem + L.zero))[tid] = 0u;
-
-    const bool fast = fabs(a.thr) >= 0.01;
-    const float sgn = a.thr >= 0.0 ? 1.0f : -1.0f;
-    const double tq = a.thr * (double)(NPX - 1) / (double)NPX;
-    const double tk2 = tq * tq;
-    const int n_units = t.item_off[t.ntiles] * NG;
-    const int m = lane & 15, kh = lane >> 4;
-
-    for (;;) {
-        if (tid == 0) s_unit = atomicAdd(&t.tile_count[t.ntiles], 1);
-        __syncthreads();
-        const int unit = __builtin_amdgcn_readfirstlane(s_unit);
-        if (unit >= n_units) break;
-        const int item = GROUPED ? unit / NG : unit;
-        const int g = GROUPED ? unit - item * NG : 0;
-        const int4 itv = t.items[item];
-        const int tile = __builtin_amdgcn_readfirstlane(itv.x);
-        const int cb = __builtin_amdgcn_readfirstlane(itv.y);
-        const int nc = __builtin_amdgcn_readfirstlane(itv.z);
-        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
-        const int x0 = tx * MVS_TILE_W, yr0 = ty * MVS_TILE_H - WID;
-        const int vb = g * kGroupViews;
-        const int GV = GROUPED ? min(kGroupViews, V - vb) : V;
-
-        // ---- 1. the tile's window region of every view of the group ----
-        for (int k = tid; k < GV * ROWS * 2; k += kMmaThreads) {
-            const int h = k & 1, vr = k >> 1;
-            const int v = vr / ROWS, rho = vr - v * ROWS;
-            const int y = yr0 + rho;
-            uint4 w = make_uint4(0u, 0u, 0u, 0u);
-            if (y >= 0 && y < sc.H)
-                w = load_signed(sc.gv + ((int64_t)(vb + v) * sc.H + y) * sc.Wp + (x0 - 8) + 16 * h);
-            *(uint4*)(reg + v * VS + rho * 32 + 16 * h) = w;
-        }
-        if constexpr (GROUPED) {
-            // the reference view is usually in another group: stage each
-            // candidate's own reference window rows
-            for (int k = tid; k < nc * NB * 2; k += kMmaThreads) {
-                const int h = k & 1, kr = k >> 1;
-                const int kk = kr / NB, j = kr - kk * NB;
-                const int pk = t.sorted[cb + kk].y;
-                const int y = ty * MVS_TILE_H + ((pk >> 4) & 7) - WID + j;   // inside: the window is valid
-                *(uint4*)(areg + (kk * NB + j) * 32 + 16 * h) =
-                    load_signed(sc.gv + ((int64_t)(pk >> 7) * sc.H + y) * sc.Wp + (x0 - 8) + 16 * h);
-            }
-            for (int k = tid; k < nc; k += kMmaThreads) asum[k] = make_int2(0, 0);
-        }
-        __syncthreads();
-
-        // ---- 2. window moments of every staged view at the tile's pixels ----
-        // horizontal sums of each region row: byte prefixes by v_dot4_i32_i8,
-        // packed as (sum s^2) << 12 | (sum s + 2048)
-        for (int k = tid; k < GV * ROWS; k += kMmaThreads) {
-            const int rho = k / GV, v = k - rho * GV;
-            const uint4 lo = *(const uint4*)(reg + v * VS + rho * 32);
-            const uint4 hi = *(const uint4*)(reg + v * VS + rho * 32 + 16);
-            const int d[8] = {(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w,
-                              (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-            int PS[33], PQ[33];
-            PS[0] = 0;
-            PQ[0] = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                PS[4 * j + 1] = __builtin_amdgcn_sdot4(d[j], 0x00000001, PS[4 * j], false);
-                PS[4 * j + 2] = __builtin_amdgcn_sdot4(d[j], 0x00000101, PS[4 * j], false);
-                PS[4 * j + 3] = __builtin_amdgcn_sdot4(d[j], 0x00010101, PS[4 * j], false);
-                PS[4 * j + 4] = __builtin_amdgcn_sdot4(d[j], 0x01010101, PS[4 * j], false);
-                PQ[4 * j + 1] = __builtin_amdgcn_sdot4(d[j] & 0xff, d[j], PQ[4 * j], false);
-                PQ[4 * j + 2] = __builtin_amdgcn_sdot4(d[j] & 0xffff, d[j], PQ[4 * j], false);
-                PQ[4 * j + 3] = __builtin_amdgcn_sdot4(d[j] & 0xffffff, d[j], PQ[4 * j], false);
-                PQ[4 * j + 4] = __builtin_amdgcn_sdot4(d[j], d[j], PQ[4 * j], false);
-            }
-            uint32_t* hrow = htmp + rho * 16 * VP + v;
-#pragma unroll
-            for (int x = 0; x < 16; ++x) {
-                const int s = PS[x + C0 + NB] - PS[x + C0];
-                const int q = PQ[x + C0 + NB] - PQ[x + C0];
-                hrow[x * VP] = ((uint32_t)q << 12) | (uint32_t)(s + 2048);
-            }
-        }
-        if constexpr (GROUPED) {
-            // the reference windows' S_a, S_aa (one row per thread, LDS atomics)
-            for (int k = tid; k < nc * NB; k += kMmaThreads) {
-                const int kk = k / NB, j = k - kk * NB;
-                const int qrel = t.sorted[cb + kk].y & 15;
-                const uint32_t wm = ((1u << NB) - 1u) << (qrel + C0);
-                const uint4 lo = *(const uint4*)(areg + (kk * NB + j) * 32);
-                const uint4 hi = *(const uint4*)(areg + (kk * NB + j) * 32 + 16);
-                const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-                int s = 0, q = 0;
-#pragma unroll
-                for (int jj = 0; jj < 8; ++jj) {
-                    const int dm = (int)(d[jj] & byte_mask((wm >> (4 * jj)) & 15u));
-                    s = __builtin_amdgcn_sdot4(dm, 0x01010101, s, false);
-                    q = __builtin_amdgcn_sdot4(dm, dm, q, false);
-                }
-                atomicAdd(&asum[kk].x, s);
-                atomicAdd(&asum[kk].y, q);
-            }
-        }
-        __syncthreads();
-        // vertical sums -> {S_b, n S_bb - S_b^2} per (pixel, view); the table
-        // overwrites the horizontal sums, so every thread reads first
-        int2 mv[MVS_TILE_H];
-        const bool m2 = tid < GV * 16;
-        const int m2x = tid / GV, m2v = tid - m2x * GV;
-        if (m2) {
-            int S[ROWS], Q[ROWS];
-#pragma unroll
-            for (int rho = 0; rho < ROWS; ++rho) {
-                const uint32_t h = htmp[(rho * 16 + m2x) * VP + m2v];
-                S[rho] = (int)(h & 0xfffu) - 2048;
-                Q[rho] = (int)(h >> 12);
-            }
-            int s = 0, q = 0;
-#pragma unroll
-            for (int rho = 0; rho < NB; ++rho) {
-                s += S[rho];
-                q += Q[rho];
-            }
-#pragma unroll
-            for (int y = 0; y < MVS_TILE_H; ++y) {
-                if (y > 0) {
-                    s += S[y + NB - 1] - S[y - 1];
-                    q += Q[y + NB - 1] - Q[y - 1];
-                }
-                mv[y] = make_int2(s, NPX * q - s * s);
-            }
-        }
-        __syncthreads();
-        if (m2)
-#pragma unroll
-            for (int y = 0; y < MVS_TILE_H; ++y) mom[(y * 16 + m2x) * VP + m2v] = mv[y];
-        __syncthreads();
-
-        // ---- 3. + 4. the candidates, 16 per wave and M-block ----
-        const int nblk = (nc + 15) >> 4;
-        for (int blk = wave; blk < nblk; blk += kMmaWaves) {
-            const int kk = blk * 16 + m;
-            const bool valid = kk < nc;
-            const int2 e = valid ? t.sorted[cb + kk] : make_int2(-1, 0);
-            const int qrel = e.y & 15, rrel = (e.y >> 4) & 7, R = e.y >> 7;
-            // A: the reference window, masked to candidate m's window columns
-            // (this lane's 16 columns) and rows (K-step rows in the window)
-            const uint32_t wm = valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u;
-            const uint32_t hm = wm >> (16 * (kh & 1));
-            uint32_t cm[4];
-#pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) cm[k4] = byte_mask((hm >> (4 * k4)) & 15u);
-            const uint32_t rb = valid ? (((1u << NB) - 1u) << rrel) >> (kh >> 1) : 0u;
-            const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
-            const int aoff = GROUPED ? L.areg + (kk * NB - rrel) * 32 + lofs : L.reg + R * VS + lofs;
-            int boff[NBLK];
-#pragma unroll
-            for (int nb = 0; nb < NBLK; ++nb) boff[nb] = L.reg + min(16 * nb + m, GV - 1) * VS + lofs;
-            v4i C[NBLK];
-#pragma unroll
-            for (int nb = 0; nb < NBLK; ++nb) C[nb] = (v4i){0, 0, 0, 0};
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const bool rv = (rb >> (2 * s)) & 1u;
-                const uint4 av = *(const uint4*)(smem + (rv ? aoff + 64 * s : L.zero));
-                const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]),
-                               (int)(av.w & cm[3])};
-#pragma unroll
-                for (int nb = 0; nb < NBLK; ++nb) {
-                    const uint4 bv = *(const uint4*)(smem + boff[nb] + 64 * s);
-                    const v4i B = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
-                    C[nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, C[nb], 0, 0, 0);
-                }
-            }
-            // per-candidate constants, shared with the wave's other lanes
-            if (kh == 0) {
-                CandInfoG c;
-                c.px = rrel * 16 + qrel;
-                int Sa = 0, da = 0;
-                if (valid) {
-                    if constexpr (GROUPED) {
-                        const int2 as = asum[kk];
-                        Sa = as.x;
-                        da = NPX * as.y - as.x * as.x;
-                    } else {
-                        const int2 ma = mom[c.px * VP + R];
-                        Sa = ma.x;
-                        da = ma.y;
-                    }
-                }
-                c.R = valid ? R : -1;
-                c.Sa = Sa;
-                c.da = da;
-                c.tkda = (float)(tk2 * (double)da);
-                c.ca = da > 0 ? (double)NPX / ((double)(NPX - 1) * sqrt((double)da)) : 0.0;
-                c.idx = e.x;
-                ci[m] = c;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            // lane (kh, m) holds C[4 kh + i][16 nb + m]: candidate 4 kh + i, view 16 nb + m
-            uint64_t P[4][NBLK], Gd[4];
-            double sacc[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const CandInfoG c = ci[4 * kh + i];
-                double sa = 0.0;
-                Gd[i] = 0;
-#pragma unroll
-                for (int nb = 0; nb < NBLK; ++nb) {
-                    const int vl = 16 * nb + m;
-                    const int2 mb = mom[c.px * VP + vl];
-                    const int num = __mul24(NPX, C[nb][i]) - __mul24(c.Sa, mb.x);
-                    const bool liv = vl < GV && vb + vl != c.R;
-                    bool pass = false, guard = false;
-                    if (fast) {
-                        const float Lf = (float)num;
-                        const float rhs = c.tkda * (float)mb.y;
-                        const float dd = fmaf(Lf, fabsf(Lf), -sgn * rhs);
-                        pass = liv && dd > 0.0f;
-                        guard = liv && fabsf(dd) < 2e-6f * rhs;
-                    } else if (liv && c.da > 0 && mb.y > 0) {
-                        const double ncc = ((double)num * (double)NPX) /
-                                           ((double)(NPX - 1) * sqrt((double)c.da * (double)mb.y));
-                        guard = fabs(ncc - a.thr) <= kGuard;
-                        pass = ncc > a.thr;
-                    }
-                    P[i][nb] = __ballot(pass);
-                    Gd[i] |= __ballot(guard);
-                    if (a.avg != nullptr && P[i][nb] != 0 && pass) {
-                        const double D = (double)mb.y;
-                        double y = __builtin_amdgcn_rsq(D);
-                        y = y * (1.5 - 0.5 * D * y * y);
-                        y = y * (1.5 - 0.5 * D * y * y);
-                        sa += (double)num * c.ca * y;
-                    }
-                }
-                sacc[i] = sa;
-            }
-            if (a.avg != nullptr) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) sacc[i] = row_sum16(sacc[i]);
-                if (m == 0)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) wsum[4 * kh + i] = sacc[i];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if (kh == 0 && valid) {
-                // candidate m = 4 j + i: its 16 bits of ballot (i, nb) sit at 16 j
-                const int j = m >> 2, i = m & 3;
-                uint64_t mk = 0;
-#pragma unroll
-                for (int nb = 0; nb < NBLK; ++nb) {
-                    const uint64_t p = i == 0 ? P[0][nb] : i == 1 ? P[1][nb] : i == 2 ? P[2][nb] : P[3][nb];
-                    mk |= ((p >> (16 * j)) & 0xffffull) << (16 * nb);
-                }
-                const uint64_t gg = i == 0 ? Gd[0] : i == 1 ? Gd[1] : i == 2 ? Gd[2] : Gd[3];
-                const int cnt = __popcll(mk);
-                const double sum = a.avg != nullptr ? wsum[m] : 0.0;
-                const int64_t idx = e.x;
-                if constexpr (GROUPED) {
-                    a.mask[idx * words + g] = mk;
-                    t.part_cnt[idx * NG + g] = cnt;
-                    t.part_sum[idx * NG + g] = sum;
-                } else {
-                    a.mask[idx] = mk;
-                    a.count[idx] = cnt;
-                    if (a.avg) a.avg[idx] = cnt ? sum * c_recip.r[cnt] : 0.0;
-                }
-                if ((gg >> (16 * j)) & 0xffffull) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
-            }
-        }
-        __syncthreads();
-    }
-}
 
 // ---------------------------------------------------------------------------
 // k_score_mma (V <= 64).  A workgroup (16 waves) takes one work item (the
@@ -1383,20 +1049,471 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     }
 }
 
-// count and avg_ncc_score of every scored candidate from its view groups' partials
-__global__ void k_group_finalize(const ScoreArgs a, const TiledArgs t) {
+// ---------------------------------------------------------------------------
+// k_score_mma_v (64 < V <= 256): the views in groups of 64 (one mask word
+// each).  A workgroup takes one work item (the candidates of one 16x8 tile,
+// at most kGroupChunk of them) from the queue and scores it against every
+// view group in turn:
+//   1. (per item) each candidate's own reference window rows go to LDS by
+//      LDS-DMA (its view is usually in another group); its S_a, w_a and
+//      decision constants from them;
+//   2. (per group) D = n S_bb - S_b^2 of every (pixel, view) of the group
+//      (int32; -1 for a constant window): one thread per (pixel column, view)
+//      sums its column's window rows straight from the staged region (masked
+//      v_dot4_i32_i8) and slides them down the tile;
+//   3. (per group) wave tasks (M-block of 16 candidates, 32 views): C = sum
+//      s_R s_v and S_b = sum s_v over the window, both by
+//      v_mfma_i32_16x16x64_i8 (S_b with the window's 0/1 indicator as A);
+//      num = n C - S_a S_b; the decision num w_b > T in binary32 with
+//      w_b = v_rsq_f32(D) (guard band 2e-6 |T| as in k_score_mma), the sum
+//      of the passing num w_b with w_b refined in binary64 (one Newton step);
+//   4. (per group) each candidate's mask word, count, sum and guard flag
+//      accumulate in its thread's registers; written after the last group
+//      (guard-band candidates to k_score_fix).
+// The regions are double-buffered: group k+1's (after an item's last group,
+// the next item's first) lands by LDS-DMA while group k is scored, as do the
+// next item's candidate list and, behind group 0's phase 2, an item's
+// reference rows.  Every LDS-DMA target is a static LDS array of its own, so
+// that the compiler sees no aliasing with the tables phases 2-4 read and
+// write.  Work items come tile-major (k_tile_scan): the workgroups in flight
+// share image rows, so TLB and L2 reach over 256 views of a large image.
+// ---------------------------------------------------------------------------
+constexpr int kVTab = 68;   // D-table row pitch (int32): the per-column writes are conflict free
+
+// a candidate's constants (LDS, per item)
+struct alignas(16) CandInfoV {
+    int32_t px, R, Sa, pk;    // D-table row of its pixel (px * kVTab), reference view, -S_a, packed pixel
+    float T, gT;              // decision threshold on num w_b and its guard band
+    double ca;                // n / (n-1) * w_a
+};
+
+// dynamic LDS of k_score_mma_v (the LDS-DMA targets are static arrays)
+struct VLds {
+    int dtab, ci, rmask, rguard, rsum, total;
+};
+
+__host__ __device__ constexpr VLds v_lds() {
+    VLds L{};
+    L.dtab = 0;                                                 // [128 px][kVTab] int32
+    L.ci = L.dtab + 128 * kVTab * 4;
+    L.rmask = L.ci + kGroupChunk * (int)sizeof(CandInfoV);      // [cand][4 view blocks] u16
+    L.rguard = L.rmask + kGroupChunk * 4 * 2;                   // [cand][2 halves] u16
+    L.rsum = L.rguard + kGroupChunk * 2 * 2 + 8;                // [cand][2 halves] double (8-B aligned)
+    L.total = L.rsum + kGroupChunk * 2 * 8;
+    return L;
+}
+
+template <int WID>
+__host__ __device__ constexpr int v_static_lds() {
+    return 2 * 64 * MmaGeom<WID>::VS + 2 * kGroupChunk * 8 + kGroupChunk * MmaGeom<WID>::NB * 32 + 16;
+}
+
+// Workgroup barrier for LDS traffic: every wave's LDS operations are complete
+// first; outstanding global loads and LDS-DMA are not waited for (the fence of
+// __syncthreads would wait for them: vmcnt(0)).
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// x through an opaque copy: what is computed from it is computed where it is
+// used, not hoisted out of loops into long-lived registers
+DEV int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// byte masks of a window of NB bytes starting at byte b0 over the 4 dwords
+// from dword b0 >> 2
+template <int NB>
+DEV void window_dword_masks(int b0, uint32_t (&mk)[4]) {
+    const int e = b0 + NB;   // one past the last byte
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int base = 4 * ((b0 >> 2) + j);
+        const int lo = max(b0 - base, 0), n = min(e - base, 4) - lo;   // bytes [lo, lo + n) of dword j
+        mk[j] = n > 0 ? (uint32_t)(((1ull << (8 * n)) - 1ull) << (8 * lo)) : 0u;
+    }
+}
+
+// 1/sqrt(D) in binary64: v_rsq_f64 + one Newton step (max relative error
+// 4.1e-15 over 4M values of D < 2^31, tools/ubench/rsq_acc.hip); nan for D <= 0
+DEV double rsqrt_nr(int D) {
+    double w = __builtin_nan("");
+    if (D > 0) {
+        const double x = (double)D;
+        w = __builtin_amdgcn_rsq(x);
+        w = w * (1.5 - 0.5 * x * w * w);
+    }
+    return w;
+}
+
+template <int WID, bool FAST>
+__global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
+                                                             const int4* __restrict__ items,
+                                                             const int2* __restrict__ sorted) {
+    using G = MmaGeom<WID>;
+    constexpr int NB = G::NB, NPX = G::NPX, ROWS = G::ROWS, KS = G::KS, VS = G::VS, C0 = G::C0;
+    constexpr int RPV = VS / 32;
+    constexpr int NPIECE = 64 * RPV * 2;                                              // 16-B pieces of a region
+    constexpr int RPIECE = (NPIECE + kMmaThreads - 1) / kMmaThreads;                  // ... per thread
+    constexpr int APIECE = (kGroupChunk * NB * 2 + kMmaThreads - 1) / kMmaThreads;   // reference-row pieces
+    static_assert(kGroupChunk <= 128, "one phase-3 task per wave");
+    // LDS-DMA targets: two regions, two candidate lists, the reference rows
+    __shared__ __attribute__((aligned(16))) uint8_t s_rg0[64 * VS], s_rg1[64 * VS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cd0[kGroupChunk * 8], s_cd1[kGroupChunk * 8];
+    __shared__ __attribute__((aligned(16))) uint8_t s_areg[kGroupChunk * NB * 32];
+    __shared__ int s_item;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr VLds L = v_lds();
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int V = sc.V;
     const int NG = t.groups;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        if (t.cand_key[i] < 0) continue;     // invalid window: k_bin wrote the outputs
-        int cnt = 0;
-        double sum = 0.0;
-        for (int g = 0; g < NG; ++g) {
-            cnt += t.part_cnt[i * NG + g];
-            sum += t.part_sum[i * NG + g];
+    const int words = (V + 63) >> 6;
+    int32_t* dtab = (int32_t*)(smem + L.dtab);
+    CandInfoV* ci = (CandInfoV*)(smem + L.ci);
+    uint16_t* rmask = (uint16_t*)(smem + L.rmask);
+    uint16_t* rguard = (uint16_t*)(smem + L.rguard);
+    double* rsum = (double*)(smem + L.rsum);
+    const double kn = (double)NPX / (double)(NPX - 1);
+    const float tqf = (float)(a.thr / kn);
+    const int n_items = t.item_off[t.ntiles];
+    int32_t* head = &t.tile_count[t.ntiles];
+
+    // region piece k (view k / 2RPV, row, half) of view group g at a tile: its
+    // gv address; rows outside the image are clamped (their pixels are never
+    // in a valid window), views past V repeat the last (never used)
+    auto region_src = [&](int tile, int g, int k) -> const uint8_t* {
+        const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
+        const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
+        const int y = min(max(ty * MVS_TILE_H - WID + (r2 >> 1), 0), sc.H - 1);
+        const int view = min(g * 64 + v, V - 1);
+        return sc.gv + ((int64_t)view * sc.H + y) * sc.Wp + (tx * MVS_TILE_W - 8) + 16 * (r2 & 1);
+    };
+    auto stage_region = [&](int tile, int g, auto bufc) {
+        uint8_t* dst = decltype(bufc)::value ? s_rg1 : s_rg0;
+        const int tv = opaque(tid);   // per-lane addressing recomputed here, not held across the loop
+#pragma unroll
+        for (int p = 0; p < RPIECE; ++p) {
+            const int k = tv + p * kMmaThreads;
+            if (k < NPIECE)
+                __builtin_amdgcn_global_load_lds((const void*)region_src(tile, g, k),
+                                                 (void __attribute__((address_space(3)))*)(dst + (p * kMmaThreads + wave * 64) * 16),
+                                                 16, 0, 0);
         }
-        a.count[i] = cnt;
-        if (a.avg) a.avg[i] = cnt ? sum * (1.0 / (double)cnt) : 0.0;
+    };
+    auto stage_cands = [&](const int4 d, auto bufc) {
+        const int32_t* csrc = (const int32_t*)(sorted + d.y);
+        if (tid < 2 * d.z)
+            __builtin_amdgcn_global_load_lds((const void*)(csrc + tid),
+                                             (void __attribute__((address_space(3)))*)((decltype(bufc)::value ? s_cd1 : s_cd0) + wave * 64 * 4),
+                                             4, 0, 0);
+    };
+
+    // the first item: its candidates and group 0's region
+    if (tid == 0) s_item = atomicAdd(head, 1);
+    __syncthreads();
+    int item = __builtin_amdgcn_readfirstlane(s_item);
+    if (item >= n_items) return;
+    int4 d = items[item];
+    stage_cands(d, std::integral_constant<int, 0>{});
+    stage_region(d.x, 0, std::integral_constant<int, 0>{});
+    __syncthreads();
+    int par = 0;     // candidate-list buffer of this item
+    int kpar = 0;    // region buffer of this group (groups alternate across items)
+
+    for (;;) {
+        const int tile = d.x, nc = d.z;
+        const int ty = tile / t.ntx;
+        const int x0 = (tile - ty * t.ntx) * MVS_TILE_W;
+        const int2* cand = (const int2*)(par ? s_cd1 : s_cd0);
+        const int my_idx = tid < nc ? cand[tid].x : 0;
+        // ---- 1. the candidates' reference rows (they land behind phase 2) ----
+        // (the candidate entries are read first: an LDS read between two
+        // LDS-DMA issues would wait for the first)
+        const int tv = opaque(tid);
+        int pks[APIECE];
+#pragma unroll
+        for (int p = 0; p < APIECE; ++p) {
+            const int k = tv + p * kMmaThreads;
+            pks[p] = k < nc * NB * 2 ? cand[k / (2 * NB)].y : 0;
+        }
+#pragma unroll
+        for (int p = 0; p < APIECE; ++p) {
+            const int k = tv + p * kMmaThreads;
+            if (k < nc * NB * 2) {
+                const int kk = k / (2 * NB), r2 = k - kk * (2 * NB);
+                const int pk = pks[p];
+                const int y = ty * MVS_TILE_H + ((pk >> 4) & 7) - WID + (r2 >> 1);   // inside: the window is valid
+                const uint8_t* src = sc.gv + ((int64_t)(pk >> 7) * sc.H + y) * sc.Wp + (x0 - 8) + 16 * (r2 & 1);
+                __builtin_amdgcn_global_load_lds((const void*)src,
+                                                 (void __attribute__((address_space(3)))*)(s_areg + (p * kMmaThreads + wave * 64) * 16),
+                                                 16, 0, 0);
+            }
+        }
+
+        int next = n_items;
+        int4 dn = make_int4(0, 0, 0, 0);
+        int acnt = 0;
+        double asum = 0.0;
+        uint32_t aguard = 0;
+        uint64_t pend = 0;   // the previous group's mask word, stored during this group's phase 2
+
+        // one view group; its region is in s_rg<buf>
+        auto group = [&](const int g, auto bufc) {
+            constexpr int buf = decltype(bufc)::value;
+            // the per-lane maps, recomputed per group rather than held in
+            // registers across the item loop
+            const int tid = opaque(threadIdx.x), lane = tid & 63;
+            const int m = lane & 15, kh = lane >> 4;
+            // phase 2 map: thread = (pixel column mx, view mv); 16 columns x 4 views per wave
+            const int mx = tid & 15, mv = tid >> 4;
+            uint32_t cmk[4];
+            window_dword_masks<NB>(mx + C0, cmk);
+            const int cd0 = (mx + C0) >> 2;
+            const uint8_t* reg = buf ? s_rg1 : s_rg0;
+            STAMP(t0);
+            const int vb = g * 64;
+            const int GV = min(64, V - vb);
+            const bool last = g + 1 == NG;
+            // the next region (group g+1, or the next item's group 0) and, after
+            // the last group, the next item's candidates land during phases 3-4
+            auto prefetch = [&]() {
+                if (!last) {
+                    stage_region(tile, g + 1, std::integral_constant<int, buf ^ 1>{});
+                } else if (next < n_items) {
+                    if (par) stage_cands(dn, std::integral_constant<int, 0>{});
+                    else stage_cands(dn, std::integral_constant<int, 1>{});
+                    stage_region(dn.x, 0, std::integral_constant<int, buf ^ 1>{});
+                }
+            };
+            // the previous group's mask word: its store has this group to complete
+            // (a barrier that waits for the region's LDS-DMA waits for it too)
+            if (g > 0 && tid < nc) a.mask[(int64_t)my_idx * words + g - 1] = pend;
+            // group 0: thread 0 claims the next item; the result is in by the
+            // barrier after phase 2, which waits for the reference rows anyway
+            // (claimed inside the group loop: a VGPR loaded before the loop and
+            // read in it would make the compiler drain every load at loop entry)
+            int claim = 0;
+            if (g == 0 && tid == 0) claim = atomicAdd(head, 1);
+            // ---- 2. D of every (pixel, view) of the group ----
+            if (mv < GV) {
+                // rows in order, the window sliding down as they come: at most
+                // NB + 1 row sums live
+                int S[ROWS], Q[ROWS];
+                const uint8_t* col = reg + mv * VS + 4 * cd0;
+                int s = 0, q = 0;
+#pragma unroll
+                for (int rho = 0; rho < ROWS; ++rho) {
+                    int sr = 0, qr = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int dm = (int)(*(const uint32_t*)(col + rho * 32 + 4 * j) & cmk[j]);
+                        sr = __builtin_amdgcn_sdot4(dm, 0x01010101, sr, false);
+                        qr = __builtin_amdgcn_sdot4(dm, dm, qr, false);
+                    }
+                    S[rho] = sr;
+                    Q[rho] = qr;
+                    s += sr;
+                    q += qr;
+                    if (rho >= NB) {
+                        s -= S[rho - NB];
+                        q -= Q[rho - NB];
+                    }
+                    if (rho >= NB - 1) {
+                        const int y = rho - (NB - 1);
+                        const int D = NPX * q - s * s;   // < 2^31: n * sum s^2 <= 121 * 121 * 128^2
+                        dtab[(y * 16 + mx) * kVTab + mv] = D > 0 ? D : -1;   // -1: v_rsq_f32 gives nan, never passes
+                    }
+                    if (rho % 4 == 3) __builtin_amdgcn_sched_barrier(0);   // loads of at most 4 rows in flight
+                }
+            } else {
+#pragma unroll
+                for (int y = 0; y < MVS_TILE_H; ++y) dtab[(y * 16 + mx) * kVTab + mv] = -1;
+            }
+            STAMP(t0a);
+            // (and, group 0, the reference rows have landed; nothing else is in
+            // flight, so the LDS reads of phases 3-4 need no waits)
+            __syncthreads();
+            STAMP(t0b);
+            if (g == 0) {
+                if (tid == 0) s_item = claim;   // published by the barrier below
+                // the candidates' constants from their reference rows
+                if (tid < nc) {
+                    const int pk = cand[tid].y;
+                    const int qrel = pk & 15;
+                    uint32_t amk[4];
+                    window_dword_masks<NB>(qrel + C0, amk);
+                    const int ad0 = (qrel + C0) >> 2;
+                    int s = 0, q = 0;
+#pragma unroll
+                    for (int j = 0; j < NB; ++j)
+#pragma unroll
+                        for (int k4 = 0; k4 < 4; ++k4) {
+                            const int dm = (int)(*(const uint32_t*)(s_areg + (tid * NB + j) * 32 + 4 * (ad0 + k4)) & amk[k4]);
+                            s = __builtin_amdgcn_sdot4(dm, 0x01010101, s, false);
+                            q = __builtin_amdgcn_sdot4(dm, dm, q, false);
+                        }
+                    const double wa = rsqrt_nr(NPX * q - s * s);
+                    CandInfoV c;
+                    c.px = (pk & 127) * kVTab;
+                    c.R = pk >> 7;
+                    c.Sa = -s;
+                    c.pk = pk;
+                    c.T = tqf * __builtin_amdgcn_rcpf((float)wa);   // nan for a constant window
+                    c.gT = 2e-6f * fabsf(c.T);
+                    c.ca = kn * wa;
+                    ci[tid] = c;
+                }
+                lds_barrier();
+                next = __builtin_amdgcn_readfirstlane(s_item);
+                if (next < n_items) dn = items[next];
+            }
+            STAMP(t1);
+            prefetch();
+            asm volatile("" ::: "memory");   // the LDS-DMA issues stay ahead of phase 3
+
+            // ---- 3. wave task (M-block b, views 32 h + [0, 32)) ----
+            const int nblk = (nc + 15) >> 4;
+            if (wave < nblk * 2) {
+                const int b = wave >> 1, h = wave & 1;
+                const int kk = b * 16 + m;
+                const bool valid = kk < nc;
+                const int pk = valid ? ci[kk].pk : 0;
+                const int qrel = pk & 15, rrel = (pk >> 4) & 7;
+                const uint32_t wm = valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u;
+                const uint32_t hm = wm >> (16 * (kh & 1));
+                uint32_t cm[4], cmi[4];
+#pragma unroll
+                for (int k4 = 0; k4 < 4; ++k4) {
+                    cm[k4] = byte_mask((hm >> (4 * k4)) & 15u);
+                    cmi[k4] = cm[k4] & 0x01010101u;
+                }
+                const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
+                // region row 2s + (kh >> 1) = window row 2s + (kh >> 1) - rrel of the candidate
+                const uint8_t* aptr = s_areg + (kk * NB - rrel) * 32 + 16 * (kh & 1);
+                const uint8_t* bptr0 = reg + min(32 * h + m, GV - 1) * VS + lofs;
+                const uint8_t* bptr1 = reg + min(32 * h + 16 + m, GV - 1) * VS + lofs;
+                v4i C0v = {0, 0, 0, 0}, C1v = {0, 0, 0, 0}, S0v = {0, 0, 0, 0}, S1v = {0, 0, 0, 0};
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const int row = 2 * s + (kh >> 1);
+                    const bool rv = valid && row >= rrel && row < rrel + NB;
+                    const uint4 av = rv ? *(const uint4*)(aptr + row * 32) : make_uint4(0u, 0u, 0u, 0u);
+                    const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]), (int)(av.w & cm[3])};
+                    const v4i AI = rv ? (v4i){(int)cmi[0], (int)cmi[1], (int)cmi[2], (int)cmi[3]} : (v4i){0, 0, 0, 0};
+                    const uint4 b0 = *(const uint4*)(bptr0 + 64 * s);
+                    const uint4 b1 = *(const uint4*)(bptr1 + 64 * s);
+                    const v4i B0 = {(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w};
+                    const v4i B1 = {(int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+                    C0v = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B0, C0v, 0, 0, 0);
+                    C1v = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B1, C1v, 0, 0, 0);
+                    S0v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B0, S0v, 0, 0, 0);
+                    S1v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B1, S1v, 0, 0, 0);
+                }
+                // lane (kh, m) holds candidate 16 b + 4 kh + i, views vb + 32 h + 16 j + m
+                uint32_t pmv = 0, gdv = 0;
+                double sacc[4];
+                static_for<4>([&](auto Ic) {
+                    constexpr int i = Ic;
+                    const CandInfoV c = ci[min(b * 16 + 4 * kh + i, nc - 1)];
+                    double sa = 0.0;
+                    uint64_t gacc = 0;
+                    static_for<2>([&](auto Jc) {
+                        constexpr int j = Jc;
+                        const int vl = 32 * h + 16 * j + m;
+                        const int D = dtab[c.px + vl];
+                        const float wf = __builtin_amdgcn_rsqf((float)D);   // nan for D = -1
+                        const int num = __mul24(c.Sa, j ? S1v[i] : S0v[i]) + __mul24(NPX, j ? C1v[i] : C0v[i]);
+                        const uint64_t liv = __builtin_amdgcn_uicmp((uint32_t)(vb + vl), (uint32_t)c.R, 33);
+                        // w_b in binary64: one Newton step from the binary32 estimate
+                        double w = (double)wf;
+                        w = w * (1.5 - 0.5 * (double)D * w * w);
+                        bool pass;
+                        uint64_t P, Gd;
+                        if constexpr (FAST) {
+                            const float x = fmaf((float)num, wf, -c.T);
+                            pass = vb + vl != c.R && x > 0.0f;
+                            P = __builtin_amdgcn_fcmpf(x, 0.0f, 2) & liv;
+                            Gd = __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4) & liv;
+                        } else {
+                            const double ncc = (double)num * w * c.ca;
+                            pass = vb + vl != c.R && ncc > a.thr;
+                            P = __ballot(pass);
+                            Gd = __ballot(vb + vl != c.R && fabs(ncc - a.thr) <= kGuard);
+                        }
+                        pmv = writelane<2 * (2 * i + j)>(pmv, (uint32_t)P);
+                        pmv = writelane<2 * (2 * i + j) + 1>(pmv, (uint32_t)(P >> 32));
+                        gacc |= Gd;
+                        sa = fma((double)num, pass ? w : 0.0, sa);
+                    });
+                    gdv = writelane<2 * i>(gdv, (uint32_t)gacc);
+                    gdv = writelane<2 * i + 1>(gdv, (uint32_t)(gacc >> 32));
+                    sacc[i] = sa;
+                    __builtin_amdgcn_sched_barrier(0);   // one candidate row at a time: register pressure
+                });
+                // candidate 16 b + l (l = 4 q + i): 16-bit piece q of ballot (i, j)
+                {
+                    const int l = lane & 15, i = l & 3, q = l >> 2;
+                    const int cc = b * 16 + l;
+                    uint32_t pc[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const uint32_t lo = __builtin_amdgcn_ds_bpermute(4 * (2 * (2 * i + j)), (int)pmv);
+                        const uint32_t hi = __builtin_amdgcn_ds_bpermute(4 * (2 * (2 * i + j) + 1), (int)pmv);
+                        pc[j] = (uint32_t)(((((uint64_t)hi << 32) | lo) >> (16 * q)) & 0xffffu);
+                    }
+                    const uint32_t glo = __builtin_amdgcn_ds_bpermute(4 * (2 * i), (int)gdv);
+                    const uint32_t ghi = __builtin_amdgcn_ds_bpermute(4 * (2 * i + 1), (int)gdv);
+                    const uint32_t gq = (uint32_t)(((((uint64_t)ghi << 32) | glo) >> (16 * q)) & 0xffffu);
+                    if (lane < 16 && cc < nc) {
+                        ((uint32_t*)rmask)[cc * 2 + h] = pc[0] | (pc[1] << 16);
+                        rguard[cc * 2 + h] = (uint16_t)gq;
+                    }
+                }
+                if (a.avg != nullptr) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sacc[i] = row_sum16(sacc[i]);
+                    const double mine = m == 0 ? sacc[0] : m == 1 ? sacc[1] : m == 2 ? sacc[2] : sacc[3];
+                    const int cc = b * 16 + 4 * kh + m;
+                    if (m < 4 && cc < nc) rsum[cc * 2 + h] = mine;
+                }
+            }
+            STAMP(t1a);
+            lds_barrier();
+            STAMP(t2);
+            // ---- 4. the group's mask word, count, sum and guard accumulate ----
+            if (tid < nc) {
+                const uint64_t mk = *(const uint64_t*)(rmask + tid * 4);   // views 16 nb + [0, 16) at bits 16 nb
+                aguard |= rguard[tid * 2] | rguard[tid * 2 + 1];
+                pend = mk;
+                acnt += __popcll(mk);
+                if (a.avg != nullptr && mk) asum += (rsum[tid * 2] + rsum[tid * 2 + 1]) * ci[tid].ca;
+            }
+            __syncthreads();   // the next region has landed
+            STAMP(t3);
+            STAMP_ADD(0, 1);
+            STAMP_ADD(1, t1 - t0);
+            STAMP_ADD(2, t2 - t1);
+            STAMP_ADD(3, t3 - t2);
+            STAMP_ADD(4, t0a - t0);    // wave 0: phase 2 own work
+            STAMP_ADD(5, t0b - t0a);   // barrier after phase 2 (group 0: the reference rows)
+            STAMP_ADD(6, t1 - t0b);    // group 0: the candidate constants
+            STAMP_ADD(7, t1a - t1);    // wave 0: prefetch issue + its phase-3 task
+        };
+        for (int g = 0; g < NG; ++g) {
+            if (kpar) group(g, std::integral_constant<int, 1>{});
+            else group(g, std::integral_constant<int, 0>{});
+            kpar ^= 1;
+        }
+        if (tid < nc) {
+            a.mask[(int64_t)my_idx * words + NG - 1] = pend;
+            a.count[my_idx] = acnt;
+            if (a.avg) a.avg[my_idx] = acnt ? asum * (1.0 / (double)acnt) : 0.0;
+            if (aguard) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)my_idx;
+        }
+        if (next >= n_items) break;
+        item = next;
+        d = dn;
+        par ^= 1;
     }
 }
 
@@ -1700,15 +1817,27 @@ template <int WID, int NBLK, bool GROUPED>
 int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s) {
     static bool attr = false;
     if constexpr (GROUPED) {
-        const MmaLdsG L = mma_lds_g<WID>(kGroupViews, 16 * NBLK, true);
-        if (!attr) {
-            if (hipFuncSetAttribute((const void*)k_score_mma_g<WID, NBLK, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, L.total) != hipSuccess)
-                return -1;
-            attr = true;
+        constexpr int lds = v_lds().total;
+        if (fabs(a->thr) >= 0.01) {
+            if (!attr) {
+                if (hipFuncSetAttribute((const void*)k_score_mma_v<WID, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+                    return -1;
+                attr = true;
+            }
+            hipLaunchKernelGGL((k_score_mma_v<WID, true>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc, *a, *t,
+                               (const int4*)t->items, (const int2*)t->sorted);
+        } else {
+            static bool attr_slow = false;
+            if (!attr_slow) {
+                if (hipFuncSetAttribute((const void*)k_score_mma_v<WID, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+                    return -1;
+                attr_slow = true;
+            }
+            hipLaunchKernelGGL((k_score_mma_v<WID, false>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc, *a, *t,
+                               (const int4*)t->items, (const int2*)t->sorted);
         }
-        hipLaunchKernelGGL((k_score_mma_g<WID, NBLK, true>), dim3(kMmaGrid), dim3(kMmaThreads), L.total, s,
-                           *sc, *a, *t);
     } else {
         // the largest table is sized for V = 16 NBLK; every V of this NBLK fits in it
         const int lds = mma_layout<WID, NBLK>(16 * NBLK).total;
@@ -1744,7 +1873,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     const bool grouped = sc->V > kGroupViews;
     if (t->tw != MVS_TILE_W || t->th != MVS_TILE_H || t->items == nullptr ||
         t->chunk != (grouped ? kGroupChunk : kMmaChunk) || t->groups != (grouped ? (sc->V + 63) / 64 : 1) ||
-        (grouped && (t->part_cnt == nullptr || t->part_sum == nullptr)) || sc->V > MVS_MAX_VIEWS)
+        sc->V > MVS_MAX_VIEWS)
         return -3;
     // tile counters, the work-queue head (tile_count[ntiles]) and fix_count:
     // left at zero by the previous batch's k_tile_scan unless zero_first
@@ -1774,7 +1903,6 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     if (rc) return rc;
     constexpr int kFixBlocks = 16;   // 64 waves: the guard list is short
     if (grouped) {
-        hipLaunchKernelGGL(k_group_finalize, dim3(nb), dim3(256), 0, s, *a, *t);
         if (sc->V <= 128)
             hipLaunchKernelGGL((k_score_fix<WID, 2>), dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
         else
@@ -1832,7 +1960,7 @@ extern "C" int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid,
 
 template <int WID>
 size_t mma_lds_bytes_w(int V) {
-    if (V > kGroupViews) return (size_t)mma_lds_g<WID>(kGroupViews, 64, true).total;
+    if (V > kGroupViews) return (size_t)(v_lds().total + v_static_lds<WID>());
     switch ((V + 15) / 16) {
         case 1: return (size_t)mma_layout<WID, 1>(V).total;
         case 2: return (size_t)mma_layout<WID, 2>(V).total;
@@ -1855,7 +1983,7 @@ extern "C" size_t mvs_mma_lds_bytes(int V, int wid) {
 extern "C" const char* mvs_timed_kernel_name(int V, int wid, int tiled) {
     (void)wid;
     if (!tiled) return "k_score";
-    return V > kGroupViews ? "k_score_mma (view groups)" : "k_score_mma";
+    return V > kGroupViews ? "k_score_mma_v" : "k_score_mma";
 }
 
 extern "C" int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,

@@ -8,6 +8,9 @@ import sys
 
 import numpy as np
 
+import faulthandler
+faulthandler.dump_traceback_later(150, exit=True)   # a stuck run names its line
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 os.environ["MVS_LIB"] = os.path.join(REPO, "simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd",
@@ -15,11 +18,19 @@ os.environ["MVS_LIB"] = os.path.join(REPO, "simple-implementation-of-structure-f
 import bench  # noqa: E402
 
 wid = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+scene = sys.argv[2] if len(sys.argv) > 2 else "dino"
 pkg = importlib.import_module(bench.PKG_NAME)
-rgb, K, R, t = bench.load_scene()
 n = 1 << 20
-c, ref = pkg.synthetic.candidates(n, K, R, t, seed=0)
+if scene == "ring256":   # k_score_mma_v: slot 0 counts (item, view group) units; 6 = phase 3 alone
+    import torch
+    rgb, K, R, t = pkg.synthetic.sphere_scene_device(256, 1080, 1920, seed=0, device=torch.device("cuda", 0))
+    c, ref = pkg.synthetic.candidates(n, K, R, t, W=1920, H=1080, seed=0)
+else:
+    rgb, K, R, t = bench.load_scene()
+    c, ref = pkg.synthetic.candidates(n, K, R, t, seed=0)
+print("scene ready", flush=True)
 ctx = pkg.MvsContext(rgb, K, R, t)
+print("context ready", flush=True)
 lib = pkg._lib.load()
 lib.mvs_read_stamps.argtypes = [ctypes.c_void_p]
 buf = np.zeros(4096 * 8, np.uint64)
@@ -33,9 +44,15 @@ items = d[:, 0]
 act = items > 0
 tot = items.sum()
 print(f"wid {wid}: workgroups with items {act.sum()}, items {tot:.0f}")
-for k, name in [(1, "staging"), (2, "moments"), (6, "  hsum"), (7, "  vsum"), (3, "candidates")]:
-    print(f"  {name:10s} {d[act, k].sum() / tot:9.0f} cycles per item")
-print(f"  wave 0: {d[act, 4].sum() / tot:9.0f} cycles of own candidate work per item, "
+labels = ([(1, "D table (+ item constants)"), (4, "  wave 0 own D-table work"), (5, "  barrier after phase 2"),
+           (6, "  item constants (group 0)"), (2, "MFMA tasks"), (7, "  wave 0 prefetch + own task"),
+           (3, "next region lands + phase 4")]
+          if scene == "ring256" else
+          [(1, "staging"), (2, "moments"), (6, "  hsum"), (7, "  vsum"), (3, "candidates")])
+for k, name in labels:
+    print(f"  {name:28s} {d[act, k].sum() / tot:9.0f} cycles per {'(item, group)' if scene == 'ring256' else 'item'}")
+if scene != "ring256":
+  print(f"  wave 0: {d[act, 4].sum() / tot:9.0f} cycles of own candidate work per item, "
       f"{d[act, 5].sum() / tot:.2f} M-blocks per item -> {d[act, 4].sum() / max(d[act, 5].sum(), 1):.0f} cycles per M-block")
 per_wg = d[act, 1] + d[act, 2] + d[act, 3]
 print(f"  per workgroup {per_wg.mean():.0f} cycles (max {per_wg.max():.0f})")
