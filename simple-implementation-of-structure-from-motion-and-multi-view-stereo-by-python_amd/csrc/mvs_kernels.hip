@@ -1285,9 +1285,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                     stage_region(dn.x, 0, std::integral_constant<int, buf ^ 1>{});
                 }
             };
-            // the previous group's mask word: its store has this group to complete
-            // (a barrier that waits for the region's LDS-DMA waits for it too)
-            if (g > 0 && tid < nc) a.mask[(int64_t)my_idx * words + g - 1] = pend;
             // group 0: thread 0 claims the next item; the result is in by the
             // barrier after phase 2, which waits for the reference rows anyway
             // (claimed inside the group loop: a VGPR loaded before the loop and
@@ -1323,7 +1320,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                         const int D = NPX * q - s * s;   // < 2^31: n * sum s^2 <= 121 * 121 * 128^2
                         dtab[(y * 16 + mx) * kVTab + mv] = D > 0 ? D : -1;   // -1: v_rsq_f32 gives nan, never passes
                     }
-                    if (rho % 4 == 3) __builtin_amdgcn_sched_barrier(0);   // loads of at most 4 rows in flight
                 }
             } else {
 #pragma unroll
@@ -1369,6 +1365,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             }
             STAMP(t1);
             prefetch();
+            // the previous group's mask word: its store has phases 3-4 to complete
+            // (the barrier after phase 4 waits for it with the region's LDS-DMA)
+            if (g > 0 && tid < nc) a.mask[(int64_t)my_idx * words + g - 1] = pend;
             asm volatile("" ::: "memory");   // the LDS-DMA issues stay ahead of phase 3
 
             // ---- 3. wave task (M-block b, views 32 h + [0, 32)) ----
@@ -1389,7 +1388,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 }
                 const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
                 // region row 2s + (kh >> 1) = window row 2s + (kh >> 1) - rrel of the candidate
-                const uint8_t* aptr = s_areg + (kk * NB - rrel) * 32 + 16 * (kh & 1);
+                const uint8_t* aptr = s_areg + (min(kk, nc - 1) * NB - rrel) * 32 + 16 * (kh & 1);
                 const uint8_t* bptr0 = reg + min(32 * h + m, GV - 1) * VS + lofs;
                 const uint8_t* bptr1 = reg + min(32 * h + 16 + m, GV - 1) * VS + lofs;
                 v4i C0v = {0, 0, 0, 0}, C1v = {0, 0, 0, 0}, S0v = {0, 0, 0, 0}, S1v = {0, 0, 0, 0};
@@ -1397,8 +1396,11 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 for (int s = 0; s < KS; ++s) {
                     const int row = 2 * s + (kh >> 1);
                     const bool rv = valid && row >= rrel && row < rrel + NB;
-                    const uint4 av = rv ? *(const uint4*)(aptr + row * 32) : make_uint4(0u, 0u, 0u, 0u);
-                    const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]), (int)(av.w & cm[3])};
+                    // an unconditional load (a row of the candidate's own, clamped), zeroed
+                    // outside the window: no branch, so the loads can run ahead
+                    const uint4 av = *(const uint4*)(aptr + min(max(row, rrel), rrel + NB - 1) * 32);
+                    const v4i A = rv ? (v4i){(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]), (int)(av.w & cm[3])}
+                                     : (v4i){0, 0, 0, 0};
                     const v4i AI = rv ? (v4i){(int)cmi[0], (int)cmi[1], (int)cmi[2], (int)cmi[3]} : (v4i){0, 0, 0, 0};
                     const uint4 b0 = *(const uint4*)(bptr0 + 64 * s);
                     const uint4 b1 = *(const uint4*)(bptr1 + 64 * s);
