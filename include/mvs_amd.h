@@ -32,6 +32,7 @@ extern "C" {
 #define MVS_E_HIP (-2)
 #define MVS_E_UNSUPPORTED (-3)
 #define MVS_E_NOMEM (-4)
+#define MVS_E_DIVZERO (-5)   /* the reference would raise ZeroDivisionError (filter_out_outlier) */
 
 typedef struct mvs_ctx mvs_ctx;
 typedef struct mvs_stage_result mvs_stage_result;
@@ -131,6 +132,26 @@ int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats);
  * [5] the whole call. */
 int mvs_stage_times(const mvs_stage_result* res, double* times);
 void mvs_stage_free(mvs_stage_result* res);
+
+/* Stage options of a context, for the stage runs that follow (mvs_stage_run,
+ * mvs_stage_begin ... mvs_stage_finish).  MVS_STAGE_FILTER_OUTLIERS runs
+ * CellTable.filter_out_outlier (MVS2.py:132-158) between the expansion and the
+ * reconstruction, as if the reference's commented-out call at MVS2.py:281
+ * were enabled (avg_ncc_score then follows the reference's arithmetic
+ * exactly).  A filled cell whose patches were all removed before it is
+ * visited makes the reference raise ZeroDivisionError: MVS_E_DIVZERO. */
+#define MVS_STAGE_FILTER_OUTLIERS 1
+/* avg_ncc_score (MVS2.py:62-76) in the reference's own arithmetic for n scored
+ * candidates (host arrays: ref, xy (n*2) and mask (n*words) as mvs_score
+ * returned them): ctNcc in numpy's order for every view of the mask, summed
+ * in view order from 0, divided by the view count (0 for an empty mask).
+ * mvs_score's avg agrees with it to 1e-12; this one is bit-exact. */
+int mvs_exact_avg(mvs_ctx* ctx, int64_t n, const int32_t* ref, const double* xy, const uint64_t* mask,
+                  int wid, double* avg);
+int mvs_stage_set_options(mvs_ctx* ctx, int flags);
+/* out[0] = outlier patches removed, out[1] = "remove a outlier" lines the
+ * reference prints for them (|V|^2 each). */
+int mvs_stage_filter_stats(const mvs_stage_result* res, int64_t* out);
 
 /* The same stage in steps, for several GPUs (one process and one context per
  * GPU).  Every rank calls mvs_stage_begin with the same inputs

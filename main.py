@@ -73,6 +73,9 @@ if __name__ == "__main__":
                         dest="seeds", default=None)
     parser.add_argument("-max_pops", help="expansion pop cap (<= 100000)", dest="max_pops",
                         default=100000, type=int)
+    parser.add_argument("--filter_outliers", dest="filter_outliers", action="store_true",
+                        help="run CellTable.filter_out_outlier before the reconstruction (the "
+                             "reference has the call commented out, MVS2.py:281)")
     parser.add_argument("-save_tracks", help="write the SfM tracks (npz) before the MVS stage",
                         dest="save_tracks", default=None)
     args = parser.parse_args()

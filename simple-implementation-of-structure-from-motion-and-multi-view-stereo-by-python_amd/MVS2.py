@@ -9,6 +9,7 @@ MyPatch.photo_consistenecy_test(...)          MVS2.py:62-77
     Same method on the same fields; one-candidate call of the batched GPU
     scorer.  Use photo_consistency_batch for many candidates.
 """
+import sys
 import time
 import zlib
 
@@ -85,7 +86,8 @@ class MyPatch(object):
         xy, mask, count, avg = ctx.score(np.asarray(self.c, np.float64)[None], [self.R], MIN_NCC, 5)
         for idx in _mask_views(mask[0]):
             self.V.append([idx, xy[0, 0], xy[0, 1]])
-        self.avg_ncc_score = float(avg[0])
+        # the reference's own sum of the passing nccs / |V| (MVS2.py:73-76), bit-exact
+        self.avg_ncc_score = float(ctx.exact_avg([self.R], xy, mask, 5)[0]) if count[0] else 0
         return self.V
 
 
@@ -111,8 +113,13 @@ def DensePointsWithMVS2(imgs, global_set, args, max_pops=100000, device=None):
 
     Under torch.distributed with world size > 1 (one process per GPU), the
     expansion sweeps are sharded across ranks (parallel.stage_sharded); every
-    rank ends with the same patches and rank 0 writes the PLY files."""
+    rank ends with the same patches and rank 0 writes the PLY files.
+
+    `args.filter_outliers` (opt-in, default off) runs CellTable.filter_out_outlier
+    (MVS2.py:132-158) before the reconstruction, as if the reference's
+    commented-out call at MVS2.py:281 were enabled, with its prints."""
     t0 = time.time()
+    filter_outliers = bool(getattr(args, "filter_outliers", False))
     par_K, par_r, par_t = read_pars(args)
     n_observations, n_world_points, legal_sets = global_set.getInfo()
     track_off, obs_view, obs_xy = tracks_to_arrays(legal_sets)
@@ -123,17 +130,25 @@ def DensePointsWithMVS2(imgs, global_set, args, max_pops=100000, device=None):
         from . import parallel
         initial, allp, stats = parallel.stage_sharded(
             ctx, track_off, obs_view, obs_xy, cell_size=args.cell_size, scale=args.scale, wid=5,
-            max_pops=max_pops, device=device)
+            max_pops=max_pops, device=device, filter_outliers=filter_outliers)
         if dist.get_rank() != 0:
             last_stats.clear()
             last_stats.update(stats)
             return None
     else:
         initial, allp, stats = ctx.stage(track_off, obs_view, obs_xy, cell_size=args.cell_size,
-                                         scale=args.scale, wid=5, max_pops=max_pops)
+                                         scale=args.scale, wid=5, max_pops=max_pops,
+                                         filter_outliers=filter_outliers)
     print("len of initial patches", len(initial))
     export2ply(initial[:, :3], initial[:, 3:], path="initial_patches")
     print("filter outliers")
+    if filter_outliers:
+        # filter_out_outlier's own prints (MVS2.py:155), one per removed Q-table entry
+        left = stats["outlier_lines"]
+        while left > 0:
+            k = min(left, 1 << 16)
+            sys.stdout.write("remove a outlier\n" * k)
+            left -= k
     print("reconstruct point cloud")
     t1 = time.time()
     print("Optimization took {0:.0f} seconds".format(t1 - t0))

@@ -57,6 +57,9 @@ SIGNATURES = [
     ("mvs_stage_rows_device", ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp]),
     ("mvs_stage_stats", ctypes.c_int, [_vp, _i64p]),
     ("mvs_stage_times", ctypes.c_int, [_vp, _dp]),
+    ("mvs_stage_set_options", ctypes.c_int, [_vp, ctypes.c_int]),
+    ("mvs_exact_avg", ctypes.c_int, [_vp, ctypes.c_int64, _i32p, _dp, _u64p, ctypes.c_int, _dp]),
+    ("mvs_stage_filter_stats", ctypes.c_int, [_vp, _i64p]),
     ("mvs_stage_free", None, [_vp]),
     ("mvs_expand_candidates", ctypes.c_int, [_vp, ctypes.c_int64, _dp, _dp, _dp, ctypes.c_int64,
                                              _i32p, _i32p, _i32p, ctypes.c_int, ctypes.c_double,
@@ -115,7 +118,14 @@ def last_error(ctx=None):
     return msg.decode() if msg else ""
 
 
+MVS_E_DIVZERO = -5
+MVS_STAGE_FILTER_OUTLIERS = 1
+
+
 def check(rc, ctx=None, what="mvs"):
+    if rc == MVS_E_DIVZERO:
+        # where the reference itself raises (filter_out_outlier, MVS2.py:144)
+        raise ZeroDivisionError(f"{what}: {last_error(ctx)}")
     if rc != 0:
         raise RuntimeError(f"{what} failed ({rc}): {last_error(ctx)}")
 
@@ -251,6 +261,19 @@ class MvsContext:
         check(rc, self._h, "mvs_score")
         return xy, mask, count, avg
 
+    def exact_avg(self, ref, xy, mask, wid=5):
+        """avg_ncc_score in the reference's arithmetic (numpy-order ctNcc, summed in
+        view order) for candidates scored by `score`: bit-exact, where score's avg
+        is within 1e-12."""
+        ref = _c(ref, np.int32).reshape(-1)
+        n = len(ref)
+        xy = _c(xy, np.float64).reshape(n, 2)
+        mask = _c(mask, np.uint64).reshape(n, self.words)
+        out = np.empty(n)
+        check(load().mvs_exact_avg(self._h, n, _p(ref, _i32p), _p(xy, _dp), _p(mask, _u64p), int(wid),
+                                   _p(out, _dp)), self._h, "mvs_exact_avg")
+        return out
+
     def score_device(self, c, ref, xy, mask, count, avg, min_ncc=0.7, wid=5, stream=None):
         """Same on device tensors (torch: pass .data_ptr() ints); stream-ordered."""
         n = int(ref.numel()) if hasattr(ref, "numel") else int(len(ref))
@@ -311,16 +334,25 @@ class MvsContext:
         check(rc, self._h, "mvs_expand_candidates")
         return X, nX, color, xy, mask, count, acc
 
-    def stage(self, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5, max_pops=100000):
-        """DensePointsWithMVS2 minus IO; returns (initial N0x6, all Nx6, stats dict)."""
+    def stage(self, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5, max_pops=100000,
+              filter_outliers=False):
+        """DensePointsWithMVS2 minus IO; returns (initial N0x6, all Nx6, stats dict).
+        filter_outliers: run CellTable.filter_out_outlier (MVS2.py:132-158) before
+        the reconstruction, as if MVS2.py:281 were enabled."""
         lib = load()
         track_off, obs_view, obs_xy = _tracks(track_off, obs_view, obs_xy)
+        self.set_stage_options(filter_outliers)
         res = _vp()
         rc = lib.mvs_stage_run(self._h, len(track_off) - 1, _p(track_off, _i64p),
                                _p(obs_view, _i32p), _p(obs_xy, _fp), int(cell_size), float(scale),
                                int(wid), int(max_pops), ctypes.byref(res))
         check(rc, self._h, "mvs_stage_run")
         return _take_result(res, self._h)
+
+    def set_stage_options(self, filter_outliers=False):
+        """Options of the stage runs that follow (mvs_stage_set_options)."""
+        flags = MVS_STAGE_FILTER_OUTLIERS if filter_outliers else 0
+        check(load().mvs_stage_set_options(self._h, flags), self._h, "mvs_stage_set_options")
 
     def stage_begin(self, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5,
                     max_pops=100000, rank=0, world=1):
@@ -357,11 +389,14 @@ def _take_result(res, h):
         check(lib.mvs_stage_stats(res, _p(st, _i64p)), h, "mvs_stage_stats")
         tm = np.empty(6)
         check(lib.mvs_stage_times(res, _p(tm, _dp)), h, "mvs_stage_times")
+        fl = np.empty(2, np.int64)
+        check(lib.mvs_stage_filter_stats(res, _p(fl, _i64p)), h, "mvs_stage_filter_stats")
     finally:
         lib.mvs_stage_free(res)
     stats = dict(zip(STAGE_STATS, (int(x) for x in st)))
     stats["times"] = dict(zip(STAGE_TIMES, (float(x) for x in tm)))
     stats["times"]["rows_to_host_s"] = t_rows
+    stats["outliers_removed"], stats["outlier_lines"] = int(fl[0]), int(fl[1])
     return out[0], out[1], stats
 
 

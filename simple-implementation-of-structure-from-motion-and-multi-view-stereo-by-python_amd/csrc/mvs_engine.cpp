@@ -291,6 +291,7 @@ void projection_matrix(const double* K, const double* R, const double* t, double
 
 struct mvs_ctx {
     int device = 0;
+    int stage_flags = 0;   // mvs_stage_set_options
     int V = 0, H = 0, W = 0, Wq = 0;
     hipStream_t stream = nullptr;
     std::vector<CamDev> cams;
@@ -360,6 +361,7 @@ struct mvs_stage_result {
     int64_t n_init = 0, n_all = 0;
     int64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     double times[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // mvs_stage_times
+    int64_t filt[2] = {0, 0};                      // mvs_stage_filter_stats
 };
 
 namespace {
@@ -519,6 +521,7 @@ struct Engine {
 
     std::vector<uint64_t> table;    // [nci][ncj][words] view bitmasks, 1 = vacant (CellTable)
     std::vector<int32_t> events;    // accepted patch objects, in fill order
+    int64_t n_accepted = -1;        // events before filter_outliers (-1: not filtered)
     int64_t n_seeds = 0;
     int64_t stat_tests = 0, stat_scored = 0, stat_sweeps = 0, stat_seed_cands = 0;
 
@@ -902,6 +905,112 @@ struct Engine {
     // the row gather (k_gather_rows) into the result's HBM rows.
     double t_out[5] = {0, 0, 0, 0, 0};   // upload, keys + sort, rows, -, end stamp (MVS_STAGE_TIMES)
     DevBuf<int32_t> o_ev, o_vals, o_init;
+
+    // CellTable.filter_out_outlier (MVS2.py:132-158) as if MVS2.py:281 ran it,
+    // between the expansion and reconstruct_from_Q.  Q_table[(v, ci, cj)] holds
+    // every accepted patch whose V list contains v, at the cell of its
+    // projection, |V| times (fill_with_point appends it once per V entry, and
+    // every V entry carries the same projection).  Keys are visited in
+    // (v, ci, cj) order; for each, threshold = sum(1 - avg) over the current
+    // list / its length, and a patch p2 of the list is an outlier if
+    // |V2|·avg2 < threshold and some other patch p1 of the list is not its
+    // neighbour (is_patch_neighbor, 0.2); outliers leave every key they are in
+    // (printing "remove a outlier" per entry: |V|² per patch).  avg_ncc_score
+    // is recomputed in the reference's arithmetic first (k_exact_avg).
+    // Patches leave whole, so the output order of the rest is unchanged.
+    void filter_outliers(mvs_stage_result* res) {
+        const int64_t nev = (int64_t)events.size();
+        n_accepted = nev;
+        if (nev == 0) return;
+        // avg_ncc_score per event, c and n per record
+        DevBuf<int32_t> d_ids;
+        DevBuf<double> d_avg;
+        d_ids.alloc(nev);
+        d_avg.alloc(nev);
+        HIPCHK(hipMemcpyAsync(d_ids.p, events.data(), nev * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        if (mvs_launch_exact_avg(&ctx->sc, recs(), wid, d_ids.p, nev, d_avg.p, s) != 0)
+            throw Fail{MVS_E_HIP, "exact_avg launch failed"};
+        std::vector<double> avg(nev), hc(nrec * 3), hn(nrec * 3);
+        HIPCHK(hipMemcpyAsync(avg.data(), d_avg.p, nev * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hc.data(), d_c.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hn.data(), d_n.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        // (key, event) entries, key = (v * nci + ci) * ncj + cj; events in fill order
+        std::vector<std::pair<int64_t, int32_t>> ent;
+        for (int64_t e = 0; e < nev; ++e) {
+            const int64_t r = events[e];
+            const int cx = h_cell[2 * r], cy = h_cell[2 * r + 1];
+            if (cx < 0 || cx >= nci || cy < 0 || cy >= ncj) continue;
+            for (int w = 0; w < words; ++w)
+                for (uint64_t m = h_mask[r * words + w]; m; m &= m - 1) {
+                    const int v = 64 * w + __builtin_ctzll(m);
+                    ent.push_back({((int64_t)v * nci + cx) * ncj + cy, (int32_t)e});
+                }
+        }
+        std::sort(ent.begin(), ent.end());
+        std::vector<uint8_t> alive(nev, 1);
+        auto cnt = [&](int32_t e) { return h_count[events[e]]; };
+        // is_patch_neighbor(p1, p2, 0.2) (MVS2.py:298-299), numpy's 3-element dots
+        auto neighbor = [&](int32_t e1, int32_t e2) {
+            const double* c1 = &hc[3 * (int64_t)events[e1]];
+            const double* c2 = &hc[3 * (int64_t)events[e2]];
+            const double* n1 = &hn[3 * (int64_t)events[e1]];
+            const double* n2 = &hn[3 * (int64_t)events[e2]];
+            const double d0 = c1[0] - c2[0], d1 = c1[1] - c2[1], d2 = c1[2] - c2[2];
+            return std::fabs(fma_dot3(d0, d1, d2, n1[0], n1[1], n1[2]) + fma_dot3(d0, d1, d2, n2[0], n2[1], n2[2])) < 0.2;
+        };
+        std::vector<int32_t> L, out;
+        int64_t removed = 0, lines = 0;
+        for (size_t b = 0; b < ent.size();) {
+            size_t e_end = b;
+            while (e_end < ent.size() && ent[e_end].first == ent[b].first) ++e_end;
+            L.clear();
+            double thr = 0.0;
+            int64_t len = 0;
+            for (size_t k = b; k < e_end; ++k) {
+                const int32_t e = ent[k].second;
+                if (!alive[e]) continue;
+                L.push_back(e);
+                const int m = cnt(e);
+                for (int i = 0; i < m; ++i) thr += 1.0 - avg[e];
+                len += m;
+            }
+            if (len == 0) {
+                const int64_t key = ent[b].first;
+                char msg[200];
+                std::snprintf(msg, sizeof msg,
+                              "filter_out_outlier: ZeroDivisionError (MVS2.py:144): every patch of filled cell "
+                              "(view %lld, %lld, %lld) was removed before it was visited",
+                              (long long)(key / ((int64_t)nci * ncj)), (long long)(key / ncj % nci),
+                              (long long)(key % ncj));
+                throw Fail{MVS_E_DIVZERO, msg};
+            }
+            thr /= (double)len;
+            out.clear();
+            for (int32_t p2 : L) {
+                if (!((double)cnt(p2) * avg[p2] < thr)) continue;
+                for (int32_t p1 : L)
+                    if (p1 != p2 && !neighbor(p1, p2)) {
+                        out.push_back(p2);
+                        break;
+                    }
+            }
+            for (int32_t p : out)
+                if (alive[p]) {
+                    alive[p] = 0;
+                    ++removed;
+                    lines += (int64_t)cnt(p) * cnt(p);
+                }
+            b = e_end;
+        }
+        std::vector<int32_t> kept;
+        kept.reserve(nev - removed);
+        for (int64_t e = 0; e < nev; ++e)
+            if (alive[e]) kept.push_back(events[e]);
+        events.swap(kept);
+        res->filt[0] = removed;
+        res->filt[1] = lines;
+    }
     DevBuf<uint64_t> o_keys, o_keys_s;
     DevBuf<uint8_t> o_tmp;
 
@@ -960,7 +1069,7 @@ struct Engine {
         }
         res->stats[0] = stat_pops;
         res->stats[1] = stat_tests;
-        res->stats[2] = (int64_t)events.size();
+        res->stats[2] = n_accepted >= 0 ? n_accepted : (int64_t)events.size();
         res->stats[3] = stat_queue_left;
         res->stats[4] = stat_scored;
         res->stats[5] = stat_sweeps;
@@ -1010,6 +1119,7 @@ void finish_engine(mvs_ctx* ctx, Engine* E, mvs_stage_result* res) {
     HIPCHK(hipMemcpyAsync(&h, ctx->d_exact.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     const double t = Engine::now();
+    if (ctx->stage_flags & MVS_STAGE_FILTER_OUTLIERS) E->filter_outliers(res);
     E->output(res);
     E->t_out[4] = Engine::now() - t;
     res->stats[7] = h;
@@ -1381,6 +1491,47 @@ int mvs_stage_stats(const mvs_stage_result* res, int64_t* stats) {
 int mvs_stage_times(const mvs_stage_result* res, double* times) {
     if (!res || !times) return MVS_E_ARG;
     std::memcpy(times, res->times, 6 * sizeof(double));
+    return 0;
+}
+
+int mvs_exact_avg(mvs_ctx* ctx, int64_t n, const int32_t* ref, const double* xy, const uint64_t* mask, int wid,
+                  double* avg) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (n < 0 || (n > 0 && (!ref || !xy || !mask || !avg))) return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
+    if (wid != 3 && wid != 5) return set_err(ctx, Fail{MVS_E_UNSUPPORTED, "exact avg supports wid 3 or 5"});
+    return guarded(ctx, [&]() {
+        for (int64_t i = 0; i < n; ++i)
+            if (ref[i] < 0 || ref[i] >= ctx->V) throw Fail{MVS_E_ARG, "ref view out of range"};
+        if (n == 0) return 0;
+        hipStream_t s = ctx->stream;
+        const int words = ctx->words();
+        ctx->s_ref.ensure(n); ctx->s_xy.ensure(n * 2); ctx->s_mask.ensure(n * words); ctx->s_avg.ensure(n);
+        HIPCHK(hipMemcpyAsync(ctx->s_ref.p, ref, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(ctx->s_xy.p, xy, n * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(ctx->s_mask.p, mask, n * words * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        RecordsDev rec{};
+        rec.R = ctx->s_ref.p;
+        rec.xy = ctx->s_xy.p;
+        rec.mask = ctx->s_mask.p;
+        if (mvs_launch_exact_avg(&ctx->sc, rec, wid, nullptr, n, ctx->s_avg.p, s) != 0)
+            throw Fail{MVS_E_HIP, "exact_avg launch failed"};
+        HIPCHK(hipMemcpyAsync(avg, ctx->s_avg.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    });
+}
+
+int mvs_stage_set_options(mvs_ctx* ctx, int flags) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (flags & ~MVS_STAGE_FILTER_OUTLIERS) return set_err(ctx, Fail{MVS_E_ARG, "unknown stage option"});
+    ctx->stage_flags = flags;
+    return 0;
+}
+
+int mvs_stage_filter_stats(const mvs_stage_result* res, int64_t* out) {
+    if (!res || !out) return MVS_E_ARG;
+    out[0] = res->filt[0];
+    out[1] = res->filt[1];
     return 0;
 }
 

@@ -170,6 +170,10 @@ int mvs_launch_event_keys(RecordsDev rec, int words, const int32_t* events, int6
                           int nci, int ncj, uint64_t* keys, hipStream_t s);
 // rows[i] = [c, rgb] of record idx[i] as float64 (the PLY rows)
 int mvs_launch_gather_rows(RecordsDev rec, const int32_t* idx, int64_t n, double* rows, hipStream_t s);
+// avg_ncc_score in the reference's arithmetic for records ids[0..n) (ids null:
+// records 0..n-1; reads R, xy, mask only) (wid 3 or 5)
+int mvs_launch_exact_avg(const SceneDev* sc, RecordsDev rec, int wid, const int32_t* ids, int64_t n,
+                         double* out, hipStream_t s);
 // stable device sort of (key, value) pairs over the low `bits` key bits;
 // tmp == NULL sizes the scratch (*tmp_bytes)
 int mvs_sort_pairs(void* tmp, size_t* tmp_bytes, const uint64_t* keys_in, uint64_t* keys_out,

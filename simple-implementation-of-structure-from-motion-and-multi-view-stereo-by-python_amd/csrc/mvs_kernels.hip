@@ -1788,6 +1788,45 @@ __global__ void k_gather_rows(RecordsDev rec, const int32_t* __restrict__ idx, i
     }
 }
 
+// avg_ncc_score of accepted patches in the reference's own arithmetic
+// (MVS2.py:62-76, for filter_out_outlier): every view of the V list in view
+// order, ctNcc in numpy's order (exact_ncc_stack), summed left to right from
+// 0 (`self.avg_ncc_score += ncc_score`), then divided by |V|.  One wave per
+// record: the lanes score the views, lane 0 sums them in order.  ids == null:
+// records 0..n-1 (a scored batch's ref / xy / mask arrays as the records).
+template <int WID, int NS>
+__global__ __launch_bounds__(256) void k_exact_avg(const SceneDev sc, const RecordsDev rec,
+                                                   const int32_t* __restrict__ ids, int64_t n,
+                                                   double* __restrict__ out) {
+    __shared__ double s_ncc[4][64 * NS];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t k = (int64_t)blockIdx.x * 4 + w;
+    if (k >= n) return;   // uniform per wave; no block-level barrier below
+    const int64_t r = ids ? ids[k] : k;
+    const int words = (sc.V + 63) >> 6;
+    const int R = rec.R[r];
+    int q = 0, rr = 0;
+    const bool ok = py_trunc(rec.xy[2 * r], &q) && py_trunc(rec.xy[2 * r + 1], &rr);
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+        const int v = lane + 64 * sl;
+        if (ok && v < sc.V && ((rec.mask[r * words + (v >> 6)] >> (v & 63)) & 1ull))
+            s_ncc[w][v] = exact_ncc_stack<WID>(sc, R, v, q, rr);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        double sum = 0.0;
+        int cnt = 0;
+        for (int v = 0; v < sc.V; ++v)
+            if ((rec.mask[r * words + (v >> 6)] >> (v & 63)) & 1ull) {
+                sum = sum + s_ncc[w][v];
+                ++cnt;
+            }
+        out[k] = cnt ? sum / (double)cnt : 0.0;
+    }
+}
+
 // Records ev0 on construction and ev1 on destruction (when given): brackets
 // exactly one kernel launch on stream s.
 struct TimedLaunch {
@@ -2051,6 +2090,27 @@ extern "C" int mvs_launch_event_keys(RecordsDev rec, int words, const int32_t* e
     hipLaunchKernelGGL(k_event_keys, dim3(grid_for(n_events, 256, 4096)), dim3(256), 0, s, rec, words, events,
                        n_events, nci, ncj, keys);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int WID>
+int launch_exact_avg_w(const SceneDev* sc, RecordsDev rec, const int32_t* ids, int64_t n, double* out,
+                       hipStream_t s) {
+    const dim3 grid((unsigned)((n + 3) / 4));
+    if (sc->V <= 64) hipLaunchKernelGGL((k_exact_avg<WID, 1>), grid, dim3(256), 0, s, *sc, rec, ids, n, out);
+    else if (sc->V <= 128) hipLaunchKernelGGL((k_exact_avg<WID, 2>), grid, dim3(256), 0, s, *sc, rec, ids, n, out);
+    else hipLaunchKernelGGL((k_exact_avg<WID, 4>), grid, dim3(256), 0, s, *sc, rec, ids, n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mvs_launch_exact_avg(const SceneDev* sc, RecordsDev rec, int wid, const int32_t* ids, int64_t n,
+                                    double* out, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (sc->V > MVS_MAX_VIEWS) return -3;
+    switch (wid) {
+        case 3: return launch_exact_avg_w<3>(sc, rec, ids, n, out, s);
+        case 5: return launch_exact_avg_w<5>(sc, rec, ids, n, out, s);
+        default: return -2;
+    }
 }
 
 extern "C" int mvs_launch_gather_rows(RecordsDev rec, const int32_t* idx, int64_t n, double* rows, hipStream_t s) {

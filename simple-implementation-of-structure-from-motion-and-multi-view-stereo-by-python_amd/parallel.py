@@ -242,7 +242,7 @@ def gather_slices(out, group=None):
 
 
 def stage_sharded(ctx, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=5,
-                  max_pops=100000, group=None, device=None):
+                  max_pops=100000, group=None, device=None, filter_outliers=False):
     """DensePointsWithMVS2 minus IO on every rank of `group` (one GPU each).
 
     Returns the same (initial, all, stats) on every rank as MvsContext.stage()
@@ -251,6 +251,10 @@ def stage_sharded(ctx, track_off, obs_view, obs_xy, cell_size=2, scale=1.0, wid=
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     if device is None:
         device = torch.device("cuda", int(ctx.device))
+    if hasattr(ctx, "set_stage_options"):      # applied by every rank's finish (identical records)
+        ctx.set_stage_options(filter_outliers)
+    elif filter_outliers:
+        raise RuntimeError("this context has no stage options")
     st = ctx.stage_begin(track_off, obs_view, obs_xy, cell_size, scale, wid, max_pops, rank, world)
     try:
         while True:

@@ -11,6 +11,11 @@ Outputs (all data, no reference source):
                         ray_plane_intersection / is_patch_neighbor samples
   stage_cap{N}.npz      DensePointsWithMVS2 outputs (initial_patches,
                         all_patches rows) on dinoRing + seeds, queue capped at N pops
+  stage_filter_cap{N}.npz  the same with the reference's filter_out_outlier
+                        (MVS2.py:132-158) enabled where MVS2.py:281 has it commented
+                        out: reconstruct_from_Q (called right after, MVS2.py:285) is
+                        wrapped to run the filter first; also the number of
+                        "remove a outlier" lines it printed
 """
 import argparse
 import contextlib
@@ -177,7 +182,7 @@ def func_golden(MVS2, imgs, K, Rm, t, rng):
     return out
 
 
-def stage_golden(MVS2, imgs, tracks, cap):
+def stage_golden(MVS2, imgs, tracks, cap, with_filter=False):
     import pyntcloud
 
     class CappedQueue(_queue.Queue):
@@ -192,17 +197,33 @@ def stage_golden(MVS2, imgs, tracks, cap):
         def empty(self):
             return self.gets >= cap or super().empty()
 
+    orig_queue = MVS2.queue.Queue
     MVS2.queue.Queue = CappedQueue
+    orig_reconstruct = MVS2.CellTable.reconstruct_from_Q
+    if with_filter:
+        def reconstruct_after_filter(self):
+            self.filter_out_outlier()
+            return orig_reconstruct(self)
+        MVS2.CellTable.reconstruct_from_Q = reconstruct_after_filter
     pyntcloud.written.clear()
     t0 = time.time()
     buf = io.StringIO()
-    with contextlib.redirect_stdout(buf), np.errstate(all="ignore"):
-        MVS2.DensePointsWithMVS2(imgs, SeedSet(tracks), Args())
+    try:
+        with contextlib.redirect_stdout(buf), np.errstate(all="ignore"):
+            MVS2.DensePointsWithMVS2(imgs, SeedSet(tracks), Args())
+    finally:
+        # restored, so that a second run in this process does not subclass this
+        # run's queue (its gets would then count twice)
+        MVS2.queue.Queue = orig_queue
+        MVS2.CellTable.reconstruct_from_Q = orig_reconstruct
     dt = time.time() - t0
     ntests = buf.getvalue().count("iteration:")
-    return {"initial_patches": pyntcloud.written["initial_patches.ply"],
-            "all_patches": pyntcloud.written["all_patches.ply"],
-            "cap": np.int64(cap), "ref_seconds": np.float64(dt), "pops": np.int64(ntests)}
+    out = {"initial_patches": pyntcloud.written["initial_patches.ply"],
+           "all_patches": pyntcloud.written["all_patches.ply"],
+           "cap": np.int64(cap), "ref_seconds": np.float64(dt), "pops": np.int64(ntests)}
+    if with_filter:
+        out["removed_lines"] = np.int64(buf.getvalue().count("remove a outlier"))
+    return out
 
 
 def main():
@@ -210,6 +231,7 @@ def main():
     ap.add_argument("--func", action="store_true")
     ap.add_argument("--seeds", action="store_true")
     ap.add_argument("--stage", type=int, nargs="*", default=[])
+    ap.add_argument("--filter-stage", type=int, nargs="*", default=[])
     a = ap.parse_args()
     assert os.path.isdir(REF), "the reference is only present in the build container"
     imgs, K, Rm, t = load_dino(DATA)
@@ -229,6 +251,12 @@ def main():
         np.savez_compressed(os.path.join(HERE, f"stage_cap{cap}.npz"), **out)
         print(f"stage cap {cap}: initial {len(out['initial_patches'])} all {len(out['all_patches'])} "
               f"in {out['ref_seconds']:.1f}s")
+    for cap in a.filter_stage:
+        out = stage_golden(MVS2, imgs, seeds_to_tracks(seeds), cap, with_filter=True)
+        np.savez_compressed(os.path.join(HERE, f"stage_filter_cap{cap}.npz"), **out)
+        print(f"stage cap {cap} with filter_out_outlier: initial {len(out['initial_patches'])} "
+              f"all {len(out['all_patches'])} removed lines {int(out['removed_lines'])} "
+              f"in {out['ref_seconds']:.1f}s", flush=True)
 
 
 if __name__ == "__main__":

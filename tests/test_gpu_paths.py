@@ -9,7 +9,10 @@ against the oracle / the reference's golden vectors):
   bench's candidate distribution and through a 2,000-pop stage;
 * images wider than 2048 pixels;
 * device calls on a caller's stream followed by host calls on the context's
-  stream (the context's scratch is ordered across streams).
+  stream (the context's scratch is ordered across streams);
+* avg_ncc_score in the reference's own arithmetic (mvs_exact_avg), and the
+  opt-in filter_out_outlier mode (MVS2.py:132-158, disabled at MVS2.py:281)
+  against the reference run with the filter enabled.
 """
 import numpy as np
 import pytest
@@ -53,8 +56,51 @@ def test_mypatch_dropin_golden(pkg, dino, func_golden):
         assert len(V) == int(f["pt_count"][k])
         for e in V:
             assert e[1] == f["pt_xy"][k, 0] and e[2] == f["pt_xy"][k, 1]
-        assert abs(p.avg_ncc_score - f["pt_avg"][k]) <= AVG_TOL
+        assert p.avg_ncc_score == f["pt_avg"][k], k   # bit-exact (mvs_exact_avg)
     mvs2.clear_context_cache()
+
+
+def test_exact_avg_bit_exact(ctx, func_golden):
+    """mvs_exact_avg reproduces the reference's avg_ncc_score (MVS2.py:73-76:
+    numpy-order ctNcc of every passing view, summed in view order, / |V|) bit
+    for bit on its 300 recorded photo tests; mvs_score's own avg within 1e-12."""
+    f = func_golden
+    for thr in np.unique(f["pt_thr"]):
+        sel = f["pt_thr"] == thr
+        xy, mask, count, avg = ctx.score(f["pt_c"][sel], f["pt_R"][sel], float(thr), 5)
+        ex = ctx.exact_avg(f["pt_R"][sel], xy, mask, 5)
+        assert np.array_equal(ex, f["pt_avg"][sel])
+        np.testing.assert_allclose(avg, f["pt_avg"][sel], rtol=0, atol=AVG_TOL)
+
+
+def test_stage_filter_outliers_vs_reference(ctx, seeds):
+    """filter_out_outlier enabled (opt-in): the reference itself run with the
+    filter before reconstruct_from_Q at a 200-pop cap (tests/golden/gen_golden.py
+    --filter-stage) -- same rows, same number of "remove a outlier" lines."""
+    import os
+    from conftest import GOLDEN
+    p = os.path.join(GOLDEN, "stage_filter_cap200.npz")
+    g = dict(np.load(p))
+    ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
+                              cell_size=2, scale=10.0, wid=5, max_pops=200, filter_outliers=True)
+    assert np.array_equal(ini, g["initial_patches"])
+    assert np.array_equal(allp, g["all_patches"])
+    assert st["outlier_lines"] == int(g["removed_lines"])
+
+
+def test_stage_filter_outliers_full_run(ctx, seeds):
+    """At the reference's 100k pops the filter removes nothing and the rows are
+    the unfiltered run's: an accepted patch has |V| >= 2 views each with ncc >
+    MIN_NCC >= 0.4, so |V|·avg > 0.8 while a cell's threshold, the mean of
+    1 - avg, is < 0.6 (MVS2.py:142-148)."""
+    ini0, all0, st0 = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
+                                cell_size=2, scale=10.0, wid=5, max_pops=100000)
+    ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
+                              cell_size=2, scale=10.0, wid=5, max_pops=100000, filter_outliers=True)
+    assert st["outliers_removed"] == 0 and st["outlier_lines"] == 0
+    assert st["accepts"] == st0["accepts"]
+    assert np.array_equal(ini, ini0) and np.array_equal(allp, all0)
+    ctx.set_stage_options(False)
 
 
 def test_mypatch_context_follows_image_edits(pkg, dino):
