@@ -81,9 +81,11 @@ int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int 
 int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
                      double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
                      double* d_avg, void* stream);
-/* Kernel timing (measurement only): while enabled, every scoring call records a
- * HIP event pair on its stream immediately around the dominant scoring kernel
- * (k_score_mma for batches of >= 2048 candidates, else k_score).  enable != 0
+/* Kernel timing (measurement only): while enabled, every enable-th scoring
+ * call (enable = 1: every call) records a HIP event pair on its stream
+ * immediately around the dominant scoring kernel (k_score_mma / k_score_mma_v
+ * for batches of >= 2048 candidates, else k_score); sampling keeps the
+ * events' own stream time out of most calls of a timed loop.  enable > 0
  * resets the record and turns it on; 0 turns it off (the record stays
  * readable).  mvs_kernel_time synchronises the recorded events and returns
  * the summed kernel time and the number of timed launches; mvs_timed_kernel

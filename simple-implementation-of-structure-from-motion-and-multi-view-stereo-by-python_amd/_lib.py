@@ -226,9 +226,10 @@ class MvsContext:
         RGB images (stream-ordered; for cold-sweep timing)."""
         check(load().mvs_ctx_rebuild(self._h, stream), self._h, "mvs_ctx_rebuild")
 
-    def kernel_timing(self, enable=True):
-        """Start (reset) or stop HIP-event timing of the dominant scoring kernel."""
-        check(load().mvs_kernel_timing(self._h, 1 if enable else 0), self._h, "mvs_kernel_timing")
+    def kernel_timing(self, enable=True, every=1):
+        """Start (reset) or stop HIP-event timing of the dominant scoring kernel;
+        every = k times every k-th scoring call."""
+        check(load().mvs_kernel_timing(self._h, int(every) if enable else 0), self._h, "mvs_kernel_timing")
 
     def kernel_time(self):
         """-> (total kernel milliseconds, timed launches) since kernel_timing(True)."""

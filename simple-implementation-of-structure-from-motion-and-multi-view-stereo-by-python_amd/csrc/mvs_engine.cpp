@@ -314,8 +314,12 @@ struct mvs_ctx {
     DevBuf<int32_t> f_rows, f_pts, f_mom, f_best;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
     int tiles_clean_ntiles = -1;   // tile counters known zero for this tile count (-1: unknown)
-    // kernel timing (mvs_kernel_timing): one event pair per scoring launch
+    // kernel timing (mvs_kernel_timing): one event pair per `timing_period`-th
+    // scoring launch (an event record between two kernels costs a few us of
+    // stream time, so a timed loop samples)
     bool timing = false;
+    int timing_period = 1;
+    int64_t timing_count = 0;
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     const char* timed_name = "";   // the kernel the last timed pair bracketed
@@ -337,6 +341,7 @@ struct mvs_ctx {
     void next_events(hipEvent_t* e0, hipEvent_t* e1) {
         *e0 = *e1 = nullptr;
         if (!timing) return;
+        if (timing_count++ % timing_period) return;
         if (ev_used + 2 > ev.size()) {
             for (int k = 0; k < 2; ++k) {
                 hipEvent_t e;
@@ -1210,8 +1215,13 @@ void mvs_ctx_destroy(mvs_ctx* ctx) {
 int mvs_kernel_timing(mvs_ctx* ctx, int enable) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
     return guarded(ctx, [&]() {
+        if (enable < 0) throw Fail{MVS_E_ARG, "timing period must be >= 0"};
         ctx->timing = enable != 0;
-        if (ctx->timing) ctx->ev_used = 0;   // disabling keeps the record readable
+        if (ctx->timing) {
+            ctx->ev_used = 0;   // disabling keeps the record readable
+            ctx->timing_period = enable;
+            ctx->timing_count = 0;
+        }
         return 0;
     });
 }

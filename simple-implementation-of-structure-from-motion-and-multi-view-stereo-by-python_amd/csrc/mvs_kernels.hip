@@ -24,33 +24,20 @@
 
 namespace {
 
-// The two windows are loaded once as aligned dwords of the stack (NB rows of
-// NW+1 quads) and re-aligned in registers; the numpy-order arithmetic then
-// runs on registers.
+// ctNcc of view R's and view v's windows at (q, r) in numpy's operation order
+// (the guard-band path: rare).  The pixels are read from the stack as the
+// loops need them rather than held in registers, so that the callers
+// (k_score_fix, k_score, k_exact_avg) stay small: no scratch, cheap launches.
 template <int WID>
 __device__ __noinline__ double exact_ncc_stack(const SceneDev sc, int R, int v, int q, int r) {
-    constexpr int NB = 2 * WID + 1, NW = (NB + 3) / 4;
-    const int q0 = q - WID, o = q0 & 3;
+    constexpr int NB = 2 * WID + 1;
     const int64_t vstride = (int64_t)sc.V * 4;
-    const uint8_t* p0 = sc.stack + (int64_t)(r - WID) * sc.row_bytes + (int64_t)(q0 >> 2) * vstride;
-    uint32_t wa[NB][NW], wb[NB][NW];
-#pragma unroll
-    for (int row = 0; row < NB; ++row) {
-        uint32_t da[NW + 1], db[NW + 1];
-#pragma unroll
-        for (int j = 0; j <= NW; ++j) {
-            da[j] = *(const uint32_t*)(p0 + (int64_t)row * sc.row_bytes + j * vstride + R * 4);
-            db[j] = *(const uint32_t*)(p0 + (int64_t)row * sc.row_bytes + j * vstride + v * 4);
-        }
-#pragma unroll
-        for (int j = 0; j < NW; ++j) {
-            wa[row][j] = __builtin_amdgcn_alignbyte(da[j + 1], da[j], o);
-            wb[row][j] = __builtin_amdgcn_alignbyte(db[j + 1], db[j], o);
-        }
-    }
-    auto A = [&](int i) -> int { return (int)((wa[i / NB][(i % NB) >> 2] >> (8 * ((i % NB) & 3))) & 0xffu); };
-    auto B = [&](int i) -> int { return (int)((wb[i / NB][(i % NB) >> 2] >> (8 * ((i % NB) & 3))) & 0xffu); };
-    return exact_ncc_fixed<NB * NB>(A, B);
+    const uint8_t* base = sc.stack + (int64_t)(r - WID) * sc.row_bytes;
+    auto px = [&](int view, int i) -> int {
+        const int row = i / NB, col = q - WID + i % NB;
+        return base[(int64_t)row * sc.row_bytes + (int64_t)(col >> 2) * vstride + view * 4 + (col & 3)];
+    };
+    return exact_ncc_generic([&](int i) { return px(R, i); }, [&](int i) { return px(v, i); }, NB * NB);
 }
 
 // Binary64 DPP move (both halves), bound_ctrl: every source lane exists.
