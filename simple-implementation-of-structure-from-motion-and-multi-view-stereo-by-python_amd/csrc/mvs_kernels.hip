@@ -1929,7 +1929,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         }
     }
     if (rc) return rc;
-    constexpr int kFixBlocks = 16;   // 64 waves: the guard list is short
+    constexpr int kFixBlocks = 64;   // 256 waves, one guard-band candidate each at a time
     if (grouped) {
         if (sc->V <= 128)
             hipLaunchKernelGGL((k_score_fix<WID, 2>), dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);
