@@ -693,6 +693,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     CandInfo* ci = (CandInfo*)(smem + L.ci) + wave * 16;
     WaveSlot<NBLK>* wp = (WaveSlot<NBLK>*)(smem + L.wp) + wave;
     if (tid < 8) ((uint32_t*)(smem + L.zero))[tid] = 0u;
+    const uint8_t* zrow = smem + L.zero;
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
@@ -916,7 +917,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     #pragma unroll
                 for (int s = 0; s < KS; ++s) {
                     const bool rv = (rb >> (2 * s)) & 1u;
-                    const uint4 av = rv ? *(const uint4*)(aptr + 64 * s) : make_uint4(0u, 0u, 0u, 0u);
+                    // rows outside the window read 16 zero bytes: an address select
+                    // instead of a branch around the load
+                    const uint4 av = *(const uint4*)(rv ? aptr + 64 * s : zrow);
                     const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]),
                                    (int)(av.w & cm[3])};
     #pragma unroll
@@ -1092,7 +1095,7 @@ __host__ __device__ constexpr VLds v_lds() {
 
 template <int WID>
 __host__ __device__ constexpr int v_static_lds() {
-    return 2 * 64 * MmaGeom<WID>::VS + 2 * kGroupChunk * 8 + kGroupChunk * MmaGeom<WID>::NB * 32 + 16;
+    return 2 * 64 * MmaGeom<WID>::VS + 2 * kGroupChunk * 8 + kGroupChunk * MmaGeom<WID>::NB * 32 + 32;
 }
 
 // Workgroup barrier for LDS traffic: every wave's LDS operations are complete
@@ -1148,6 +1151,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     __shared__ __attribute__((aligned(16))) uint8_t s_cd0[kGroupChunk * 8], s_cd1[kGroupChunk * 8];
     __shared__ __attribute__((aligned(16))) uint8_t s_areg[kGroupChunk * NB * 32];
     __shared__ int s_item;
+    __shared__ uint4 s_zero;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr VLds L = v_lds();
     const int tid = threadIdx.x;
@@ -1196,7 +1200,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     };
 
     // the first item: its candidates and group 0's region
-    if (tid == 0) s_item = atomicAdd(head, 1);
+    if (tid == 0) {
+        s_item = atomicAdd(head, 1);
+        s_zero = make_uint4(0u, 0u, 0u, 0u);
+    }
     __syncthreads();
     int item = __builtin_amdgcn_readfirstlane(s_item);
     if (item >= n_items) return;
@@ -1383,11 +1390,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 for (int s = 0; s < KS; ++s) {
                     const int row = 2 * s + (kh >> 1);
                     const bool rv = valid && row >= rrel && row < rrel + NB;
-                    // an unconditional load (a row of the candidate's own, clamped), zeroed
-                    // outside the window: no branch, so the loads can run ahead
-                    const uint4 av = *(const uint4*)(aptr + min(max(row, rrel), rrel + NB - 1) * 32);
-                    const v4i A = rv ? (v4i){(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]), (int)(av.w & cm[3])}
-                                     : (v4i){0, 0, 0, 0};
+                    // rows outside the window read 16 zero bytes: an address select
+                    // instead of a branch around the load
+                    const uint4 av = *(const uint4*)(rv ? aptr + row * 32 : (const uint8_t*)&s_zero);
+                    const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]), (int)(av.w & cm[3])};
                     const v4i AI = rv ? (v4i){(int)cmi[0], (int)cmi[1], (int)cmi[2], (int)cmi[3]} : (v4i){0, 0, 0, 0};
                     const uint4 b0 = *(const uint4*)(bptr0 + 64 * s);
                     const uint4 b1 = *(const uint4*)(bptr1 + 64 * s);
