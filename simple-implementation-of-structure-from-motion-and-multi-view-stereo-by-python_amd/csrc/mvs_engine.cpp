@@ -780,25 +780,56 @@ struct Engine {
             const int32_t r = queue[qhead].rec;
             const int64_t base = h_child[r];
             if (base < 0) break;
+            // the FIFO is known ahead: pull the records a few entries on, and
+            // the children of the entries nearer, into cache (the record
+            // arrays outgrow the caches; the walk is latency-bound)
+            if (qhead + 8 < queue.size()) {
+                const int32_t r8 = queue[qhead + 8].rec;
+                __builtin_prefetch(&h_child[r8]);
+                __builtin_prefetch(&h_cell[2 * (int64_t)r8]);
+                __builtin_prefetch(&h_mask[(int64_t)r8 * words]);
+            }
+            if (qhead + 3 < queue.size()) {
+                const int64_t b3 = h_child[queue[qhead + 3].rec];
+                if (b3 >= 0) {
+                    __builtin_prefetch(&h_accept[b3]);
+                    __builtin_prefetch(&h_count[b3]);
+                }
+            }
             if (--queue[qhead].left == 0) ++qhead;
             --queued;
             ++pops;
             const long ci = h_cell[2 * r], cj = h_cell[2 * r + 1];
+            // every view of the parent tests the same four cells (ci +- 1, cj +- 1):
+            // their vacancy words are loaded once per mask word and again after
+            // a fill (is_vacant, MVS2.py:90-96; off-grid cells are never vacant)
+            const uint64_t* nb4[4];
+            for (int k = 0; k < 4; ++k) {
+                const long a = ci + ((k >> 1) ? 1 : -1), bb = cj + ((k & 1) ? 1 : -1);
+                nb4[k] = (a < 0 || a >= nci || bb < 0 || bb >= ncj) ? nullptr : &table[(a * ncj + bb) * words];
+            }
             int h = 0;
             for (int w = 0; w < words; ++w) {
+                uint64_t vw[4];
+                auto load4 = [&]() {
+                    for (int k = 0; k < 4; ++k) vw[k] = nb4[k] ? nb4[k][w] : 0ull;
+                };
+                load4();
                 uint64_t m = h_mask[(int64_t)r * words + w];
                 while (m) {
                     const int v = 64 * w + __builtin_ctzll(m);
+                    const uint64_t bit = m & (~m + 1);
                     m &= m - 1;
                     for (int i = -1; i <= 1; i += 2) {
                         const int64_t child = base + 2 * h + (i > 0 ? 1 : 0);
                         for (int j = -1; j <= 1; j += 2) {
-                            if (!vacant(v, ci + i, cj + j)) continue;
+                            if (!(vw[(i > 0 ? 2 : 0) + (j > 0 ? 1 : 0)] & bit)) continue;
                             ++stat_tests;
                             if (trace) std::fprintf(stderr, "E pop %lld rec %d v %d i %d j %d child %lld acc %d cnt %d cell %d %d\n",
                                 (long long)pops, r, v, i, j, (long long)child, (int)h_accept[child], h_count[child], h_cell[2*child], h_cell[2*child+1]);
                             if (h_accept[child]) {
                                 fill_record(child);
+                                load4();
                                 events.push_back((int32_t)child);
                                 if (h_count[child] > 0) {
                                     queue.push_back(QEntry{(int32_t)child, h_count[child]});

@@ -73,16 +73,19 @@ def test_exact_avg_bit_exact(ctx, func_golden):
         np.testing.assert_allclose(avg, f["pt_avg"][sel], rtol=0, atol=AVG_TOL)
 
 
-def test_stage_filter_outliers_vs_reference(ctx, seeds):
+@pytest.mark.parametrize("cap", [200, 1000])
+def test_stage_filter_outliers_vs_reference(ctx, seeds, cap):
     """filter_out_outlier enabled (opt-in): the reference itself run with the
-    filter before reconstruct_from_Q at a 200-pop cap (tests/golden/gen_golden.py
-    --filter-stage) -- same rows, same number of "remove a outlier" lines."""
+    filter before reconstruct_from_Q at 200- and 1000-pop caps
+    (tests/golden/gen_golden.py --filter-stage) -- same rows, same number of
+    "remove a outlier" lines."""
     import os
     from conftest import GOLDEN
-    p = os.path.join(GOLDEN, "stage_filter_cap200.npz")
+    p = os.path.join(GOLDEN, f"stage_filter_cap{cap}.npz")
     g = dict(np.load(p))
+    assert int(g["pops"]) == cap
     ini, allp, st = ctx.stage(seeds["track_off"], seeds["obs_view"], seeds["obs_xy"],
-                              cell_size=2, scale=10.0, wid=5, max_pops=200, filter_outliers=True)
+                              cell_size=2, scale=10.0, wid=5, max_pops=cap, filter_outliers=True)
     assert np.array_equal(ini, g["initial_patches"])
     assert np.array_equal(allp, g["all_patches"])
     assert st["outlier_lines"] == int(g["removed_lines"])
