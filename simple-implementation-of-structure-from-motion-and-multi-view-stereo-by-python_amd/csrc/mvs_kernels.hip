@@ -49,14 +49,23 @@ DEV double dpp_f64(double x) {
     return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// Sum over each row of 16 lanes, result in every lane of the row (the
-// additions are commutative pairs, so all lanes hold the same value).
-DEV double row_sum16(double x) {
-    x += dpp_f64<0xB1>(x);    // quad_perm [1,0,3,2]
-    x += dpp_f64<0x4E>(x);    // quad_perm [2,3,0,1]
-    x += dpp_f64<0x141>(x);   // row_half_mirror
-    x += dpp_f64<0x140>(x);   // row_mirror
-    return x;
+// Reduce-scatter of four values over each row of 16 lanes: lane m of a row
+// (m = lane & 15) returns the row sum of x[m & 3], so lanes m < 4 hold the
+// four sums.  Two partner swaps halve the values a lane carries (keep one
+// index, send the other), then two rotations sum the lanes that share the low
+// two bits: 27 VALU instead of four full row sums (48) and a select.
+DEV double row_sum16_x4(const double (&x)[4], int m) {
+    const bool b0 = m & 1, b1 = (m >> 1) & 1;
+    double k0 = b0 ? x[1] : x[0], s0 = b0 ? x[0] : x[1];
+    double k1 = b0 ? x[3] : x[2], s1 = b0 ? x[2] : x[3];
+    k0 += dpp_f64<0xB1>(s0);    // quad_perm [1,0,3,2]: index b0 (+2)
+    k1 += dpp_f64<0xB1>(s1);
+    double kk = b1 ? k1 : k0;
+    const double ss = b1 ? k0 : k1;
+    kk += dpp_f64<0x4E>(ss);    // quad_perm [2,3,0,1]: index b0 + 2 b1
+    kk += dpp_f64<0x124>(kk);   // row_ror:4
+    kk += dpp_f64<0x128>(kk);   // row_ror:8
+    return kk;
 }
 
 DEV double wave_sum(double x) {
@@ -971,8 +980,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                             // ncc > thr <=> num w_b > T; w_b nan (constant window) never passes
                             const float wf = WF ? twf[o] : (float)w;
                             const float x = fmaf((float)num, wf, -c.T);
-                            pass = vl != c.R && x > 0.0f;
                             P = __builtin_amdgcn_fcmpf(x, 0.0f, 2) & liv;                   // ogt
+                            // the lane's bit of P as the select condition of the sum
+                            // (the compares are not evaluated a second time)
+                            pass = __builtin_amdgcn_inverse_ballot_w64(P);
                             g |= __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4) & liv;           // olt
                         } else {
                             const double ncc = (double)num * w * c.ca;
@@ -991,9 +1002,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 if (lane < 2 * 4 * NBLK) wp->pm[lane] = pmv;
                 if (lane < 8) wp->gd[lane] = gdv;
                 if (a.avg != nullptr) {
-    #pragma unroll
-                    for (int i = 0; i < 4; ++i) sacc[i] = row_sum16(sacc[i]);
-                    const double mine = m == 0 ? sacc[0] : m == 1 ? sacc[1] : m == 2 ? sacc[2] : sacc[3];
+                    const double mine = row_sum16_x4(sacc, m);
                     if (m < 4) wp->wsum[4 * kh + m] = mine;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1426,8 +1435,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                         uint64_t P, Gd;
                         if constexpr (FAST) {
                             const float x = fmaf((float)num, wf, -c.T);
-                            pass = vb + vl != c.R && x > 0.0f;
                             P = __builtin_amdgcn_fcmpf(x, 0.0f, 2) & liv;
+                            pass = __builtin_amdgcn_inverse_ballot_w64(P);   // no second compare
                             Gd = __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4) & liv;
                         } else {
                             const double ncc = (double)num * w * c.ca;
@@ -1465,9 +1474,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                     }
                 }
                 if (a.avg != nullptr) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) sacc[i] = row_sum16(sacc[i]);
-                    const double mine = m == 0 ? sacc[0] : m == 1 ? sacc[1] : m == 2 ? sacc[2] : sacc[3];
+                    const double mine = row_sum16_x4(sacc, m);
                     const int cc = b * 16 + 4 * kh + m;
                     if (m < 4 && cc < nc) rsum[cc * 2 + h] = mine;
                 }
