@@ -36,6 +36,8 @@ def build(force=False, verbose=False, stamps=False):
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
     if stamps:
         cmd.append("-DMVS_STAMPS")
+    # A/B of code-generation options (e.g. "-mllvm -amdgpu-sched-strategy=iterative-ilp")
+    cmd += os.environ.get("MVS_EXTRA_FLAGS", "").split()
     cmd += ["-o", out + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
