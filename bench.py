@@ -8,8 +8,10 @@ reference's 11x11 window (wid=5, MVS2.py:64/69) at MIN_NCC 0.7.  The sweep is
 one block of a global candidate queue: rank r scores block r (seed r) of a
 queue of N x 2^20 candidates (weak scaling), or with --strong its
 shard_range slice of one 2^20 queue.  A step = score the sweep on the GPU
-(inputs resident in HBM) + the sweep's exchange: the accepted candidates
-(|V| >= 3) with their masks and 3D points all-gathered over RCCL (N > 1).
+(inputs resident in HBM) + the sweep's exchange (N > 1): the accepted
+candidates (|V| >= 3) as rows [index, mask, 3D point] packed on the device
+and all-gathered over RCCL on a second stream, overlapping the next sweep
+(parallel.PointsExchange).
 
 Beside the headline (rank 0 at N = 1 only, so that the driver's N > 1 runs
 stay short):
@@ -213,8 +215,9 @@ def main():
             if evs is not None:
                 evs[1].record(stream)
             if exchange and world > 1:
-                rec = par.exchange_accepted_points(sw["off"], sw["count"], sw["mask"], sw["c"], vlb)
-                got["n"] = int(rec.shape[0])
+                # pack (device, no host sync) + all-gather on the exchange's own
+                # stream, overlapping the next sweep (parallel.PointsExchange)
+                sw["exch"].post(sw["off"], sw["count"], sw["mask"], sw["c"], vlb, stream=stream)
 
         for _ in range(warmup):
             step()
@@ -239,6 +242,8 @@ def main():
         if kl != len(timed_steps) or kt <= 0.0:
             raise RuntimeError(f"kernel timing recorded {kl} launches / {kt} ms for {len(timed_steps)} timed steps")
         pms = sum(e0.elapsed_time(e1) for e0, e1 in evs.values()) / len(evs)
+        if exchange and world > 1:
+            got["n"] = int(sum(sw["exch"].check()))       # every rank's rows arrived, none over capacity
         if world > 1:
             tt = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -247,6 +252,15 @@ def main():
 
     sw = sweep_inputs(V, K, R, t, W, H, a.n, a.strong)
     n = sw["n"]
+    if world > 1:
+        # exchange capacity: this sweep's accepted count (one untimed score),
+        # the maximum over ranks plus a margin (rows of every rank are equal-sized)
+        ctx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], a.thr, a.wid,
+                         stream=stream.cuda_stream)
+        kk = (sw["count"] >= vlb).sum().to(torch.int64).reshape(1)
+        dist.all_reduce(kk, op=dist.ReduceOp.MAX)
+        cap = int(kk.item()) + int(kk.item()) // 16 + 256
+        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap, dev)
     total_n = a.n if a.strong else a.n * world
     dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup)
     value = total_n * a.steps / dt

@@ -81,6 +81,30 @@ int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int 
 int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
                      double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
                      double* d_avg, void* stream);
+/* CellTable.filter_out_outlier (MVS2.py:132-158) on the host, over n accepted
+ * patches in fill order (what the stage's opt-in filter mode runs between
+ * the expansion and reconstruct_from_Q): patch e has cell[2e..2e+1] =
+ * which_cell of its projection (MVS2.py:113), mask[e*words..] its V list,
+ * count[e] = |V|, avg[e] = avg_ncc_score, c[3e..], nrm[3e..].  Out:
+ * alive[e] = 0 for the removed patches, stats[0] = removed patches,
+ * stats[1] = "remove a outlier" lines the reference prints.  The
+ * reference's ZeroDivisionError (a filled cell emptied before its visit,
+ * MVS2.py:144) is MVS_E_DIVZERO.  Host pointers; no GPU needed. */
+int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* cell,
+                        const uint64_t* mask, const int32_t* count, const double* avg,
+                        const double* c, const double* nrm, uint8_t* alive, int64_t* stats);
+/* The multi-GPU sweep's exchange record set (no reference counterpart: the
+ * reference is single-process).  The accepted candidates
+ * (count >= vlb, MVS2.py:256/369) of a slice of n scored candidates are
+ * packed, in index order, into d_out[(cap + 1) * width] int64 with
+ * width = 1 + words + 3: row 0 = [accepted, n, cap, 0...], row 1 + j =
+ * [offset + i, mask words of i, x, y, z bit patterns of d_c[i]].  Device
+ * pointers, stream-ordered, no host synchronisation (the accepted total is
+ * in the header; a slice with more than cap accepted keeps its first cap).
+ * Feeds the all-gather of parallel.PointsExchange. */
+int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count,
+                      const uint64_t* d_mask, const double* d_c, int vlb, int64_t cap,
+                      int64_t* d_out, void* stream);
 /* Kernel timing (measurement only): while enabled, every enable-th scoring
  * call (enable = 1: every call) records a HIP event pair on its stream
  * immediately around the dominant scoring kernel (k_score_mma / k_score_mma_v
@@ -161,19 +185,26 @@ int mvs_stage_filter_stats(const mvs_stage_result* res, int64_t* out);
  *   nj = mvs_stage_plan(st)          commit in reference order until the FIFO
  *                                    head needs unscored children; plan the next
  *                                    sweep of nj child jobs (0: stage finished)
- *   mvs_stage_score_slice(st, out)   score this rank's contiguous slice of the
- *                                    sweep (rank r: jobs [r*b + min(r, x),
+ *   mvs_stage_score_slice(st, out)   the geometry of every child of the sweep
+ *                                    (it depends only on parent records, which
+ *                                    every rank holds) and the photo + accept
+ *                                    test of this rank's contiguous slice
+ *                                    (rank r: jobs [r*b + min(r, x),
  *                                    ... + b + (r < x)), b = nj / world,
- *                                    x = nj % world) and pack its records into
- *                                    the device buffer out[ceil(nj/world)][width]
- *                                    (world > 1; may be NULL when world == 1)
+ *                                    x = nj % world); the slice's photo-test
+ *                                    masks go to the device buffer
+ *                                    out[ceil(nj/world)][width] (world > 1;
+ *                                    may be NULL when world == 1)
  *   <all-gather the slices, e.g. RCCL>
  *   mvs_stage_ingest(st, all)        all[world][ceil(nj/world)][width] (device):
- *                                    every rank's records into the record table;
- *                                    `all` must be complete when called (the
- *                                    context's stream waits for no other stream)
+ *                                    the other ranks' masks into the record
+ *                                    table, their counts (popcount) and accept
+ *                                    tests; `all` must be complete when called
+ *                                    (the context's stream waits for no other
+ *                                    stream)
  * and ends with mvs_stage_finish (same result as mvs_stage_run) and
- * mvs_stage_destroy.  width = mvs_stage_record_width(st) int64 words.  Seeding
+ * mvs_stage_destroy.  width = mvs_stage_record_width(st) int64 words (the
+ * mask words: 8 B per child at V <= 64).  Seeding
  * is replicated on every rank; the commit is identical on every rank because
  * it reads identical records.  Calls are synchronous. */
 int mvs_stage_begin(mvs_ctx* ctx, int64_t n_tracks, const int64_t* track_off,

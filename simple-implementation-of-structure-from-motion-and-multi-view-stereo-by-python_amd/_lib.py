@@ -33,6 +33,10 @@ SIGNATURES = [
                                  _dp, _u64p, _i32p, _dp]),
     ("mvs_score_device", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int,
                                         ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
+    ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
+                                         ctypes.c_int64, _vp, _vp]),
+    ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
+                                           _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
     ("mvs_exact_hits", ctypes.c_int64, [_vp]),
     ("mvs_kernel_timing", ctypes.c_int, [_vp, ctypes.c_int]),
     ("mvs_kernel_time", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
@@ -152,6 +156,25 @@ def sfm_pair(KA, RA, tA, KB, RB, tB, q, tr, max_err):
     check(load().mvs_sfm_pair(*[_p(m, _dp) for m in mats], n, _p(q, _fp), _p(tr, _fp),
                               float(max_err), _p(pt, _fp), _p(keep, _u8p)), None, "mvs_sfm_pair")
     return pt[:n], keep[:n].astype(bool)
+
+
+def filter_outliers(cell, mask, count, avg, c, nrm, nci, ncj):
+    """CellTable.filter_out_outlier (MVS2.py:132-158) on the host over accepted
+    patches in fill order (mvs_filter_outliers): -> (alive bool (n,), removed,
+    "remove a outlier" lines).  Raises ZeroDivisionError where the reference does."""
+    cell = _c(cell, np.int32).reshape(-1, 2)
+    n = len(cell)
+    mask = _c(mask, np.uint64).reshape(n, -1)
+    count = _c(count, np.int32).reshape(n)
+    avg = _c(avg, np.float64).reshape(n)
+    c = _c(c, np.float64).reshape(n, 3)
+    nrm = _c(nrm, np.float64).reshape(n, 3)
+    alive = np.empty(max(n, 1), np.uint8)
+    stats = np.zeros(2, np.int64)
+    check(load().mvs_filter_outliers(n, mask.shape[1], int(nci), int(ncj), _p(cell, _i32p), _p(mask, _u64p),
+                                     _p(count, _i32p), _p(avg, _dp), _p(c, _dp), _p(nrm, _dp),
+                                     _p(alive, _u8p), _p(stats, _i64p)), None, "mvs_filter_outliers")
+    return alive[:n].astype(bool), int(stats[0]), int(stats[1])
 
 
 def triangulate(P1, P2, x1, x2):
@@ -284,6 +307,20 @@ class MvsContext:
                                      ptr(avg) if avg is not None else None,
                                      stream if stream is not None else None)
         check(rc, self._h, "mvs_score_device")
+
+    def pack_accepted(self, offset, count, mask, c, vlb, out, stream=None):
+        """mvs_pack_accepted: the accepted candidates (count >= vlb) of a scored
+        slice as exchange rows of out (device int64 tensor (cap + 1, 1 + words + 3):
+        row 0 = [accepted, n, cap, 0...], then [offset + i, mask words, x y z bits]
+        in index order); stream-ordered, no host sync."""
+        n = int(count.numel())
+        cap = int(out.shape[0]) - 1
+        if out.dtype.itemsize != 8 or out.shape[1] != 1 + self.words + 3 or not out.is_contiguous():
+            raise RuntimeError("pack_accepted: out must be contiguous int64 (cap + 1, 1 + words + 3)")
+        rc = load().mvs_pack_accepted(self._h, n, int(offset), count.data_ptr(), mask.data_ptr(),
+                                      c.data_ptr(), int(vlb), cap, out.data_ptr(),
+                                      stream if stream is not None else None)
+        check(rc, self._h, "mvs_pack_accepted")
 
     def harris_points(self, view):
         """getHarrisPoints(imgs[view]) (HarrisFeatures.py:135-161) on the GPU:

@@ -307,6 +307,8 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand;
+    // mvs_pack_accepted: accepted count per 1024-candidate chunk
+    DevBuf<int32_t> p_chunk;
     DevBuf<int4> t_items;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
     DevBuf<float> f_resp, f_dil;
@@ -498,6 +500,91 @@ void expand_device(mvs_ctx* ctx, const RecordsDev& r, const ExpandArgs& a, int w
     score_device(ctx, a.n, r.c + 3 * f, r.R + f, wid, a.thr, r.xy + 2 * f, r.mask + words * f, r.count + f,
                  nullptr, s);
     if (mvs_launch_expand_accept(r, &a, s) != 0) throw Fail{MVS_E_HIP, "expand_accept launch failed"};
+}
+
+// CellTable.filter_out_outlier (MVS2.py:132-158) over n accepted patches in
+// fill order (patch e: cell = which_cell of its projection, V-list mask,
+// |V| = count, avg_ncc_score, centre, normal).  Q_table[(v, ci, cj)] holds
+// patch e |V| times for every v of its V list at its one cell (every V entry
+// carries the same projection, MVS2.py:105-107); keys are visited in
+// (v, ci, cj) order; threshold = sum of (1 - avg) over the key's current
+// list / its length (a filled cell whose list emptied raises
+// ZeroDivisionError, MVS2.py:144 -> MVS_E_DIVZERO); a patch p2 of the list
+// is an outlier if |V2| avg2 < threshold and some other patch p1 of the list
+// is not its neighbour (is_patch_neighbor, 0.2, MVS2.py:298-299); outliers
+// leave every key (|V|^2 "remove a outlier" lines each).  alive[e] = 0 for
+// the removed.
+void filter_outliers_core(int64_t n, int words, int nci, int ncj, const int32_t* cell, const uint64_t* mask,
+                          const int32_t* count, const double* avg, const double* c, const double* nrm,
+                          uint8_t* alive, int64_t* removed_out, int64_t* lines_out) {
+    // (key, patch) entries, key = (v * nci + ci) * ncj + cj; patches in fill order
+    std::vector<std::pair<int64_t, int32_t>> ent;
+    for (int64_t e = 0; e < n; ++e) {
+        alive[e] = 1;
+        const int cx = cell[2 * e], cy = cell[2 * e + 1];
+        if (cx < 0 || cx >= nci || cy < 0 || cy >= ncj) continue;
+        for (int w = 0; w < words; ++w)
+            for (uint64_t m = mask[e * words + w]; m; m &= m - 1) {
+                const int v = 64 * w + __builtin_ctzll(m);
+                ent.push_back({((int64_t)v * nci + cx) * ncj + cy, (int32_t)e});
+            }
+    }
+    std::sort(ent.begin(), ent.end());
+    // is_patch_neighbor(p1, p2, 0.2) (MVS2.py:298-299), numpy's 3-element dots
+    auto neighbor = [&](int32_t e1, int32_t e2) {
+        const double* c1 = &c[3 * (int64_t)e1];
+        const double* c2 = &c[3 * (int64_t)e2];
+        const double* n1 = &nrm[3 * (int64_t)e1];
+        const double* n2 = &nrm[3 * (int64_t)e2];
+        const double d0 = c1[0] - c2[0], d1 = c1[1] - c2[1], d2 = c1[2] - c2[2];
+        return std::fabs(fma_dot3(d0, d1, d2, n1[0], n1[1], n1[2]) + fma_dot3(d0, d1, d2, n2[0], n2[1], n2[2])) < 0.2;
+    };
+    std::vector<int32_t> L, out;
+    int64_t removed = 0, lines = 0;
+    for (size_t b = 0; b < ent.size();) {
+        size_t e_end = b;
+        while (e_end < ent.size() && ent[e_end].first == ent[b].first) ++e_end;
+        L.clear();
+        double thr = 0.0;
+        int64_t len = 0;
+        for (size_t k = b; k < e_end; ++k) {
+            const int32_t e = ent[k].second;
+            if (!alive[e]) continue;
+            L.push_back(e);
+            const int m = count[e];
+            for (int i = 0; i < m; ++i) thr += 1.0 - avg[e];
+            len += m;
+        }
+        if (len == 0) {
+            const int64_t key = ent[b].first;
+            char msg[200];
+            std::snprintf(msg, sizeof msg,
+                          "filter_out_outlier: ZeroDivisionError (MVS2.py:144): every patch of filled cell "
+                          "(view %lld, %lld, %lld) was removed before it was visited",
+                          (long long)(key / ((int64_t)nci * ncj)), (long long)(key / ncj % nci),
+                          (long long)(key % ncj));
+            throw Fail{MVS_E_DIVZERO, msg};
+        }
+        thr /= (double)len;
+        out.clear();
+        for (int32_t p2 : L) {
+            if (!((double)count[p2] * avg[p2] < thr)) continue;
+            for (int32_t p1 : L)
+                if (p1 != p2 && !neighbor(p1, p2)) {
+                    out.push_back(p2);
+                    break;
+                }
+        }
+        for (int32_t p : out)
+            if (alive[p]) {
+                alive[p] = 0;
+                ++removed;
+                lines += (int64_t)count[p] * count[p];
+            }
+        b = e_end;
+    }
+    *removed_out = removed;
+    *lines_out = lines;
 }
 
 // ---------------------------------------------------------------------------
@@ -884,9 +971,7 @@ struct Engine {
         return sweep_n;
     }
 
-    // k_expand over jobs [b, e) of the planned sweep -> records sweep_first + [b, e)
-    void score_range(int64_t b, int64_t e) {
-        if (e <= b) return;
+    ExpandArgs sweep_args(int64_t b, int64_t e) {
         ExpandArgs a{};
         a.n = e - b;
         a.first_out = sweep_first + b;
@@ -896,7 +981,41 @@ struct Engine {
         a.dist_thr = 0.05 / scale;
         a.thr = 0.7;
         a.exact_hits = ctx->d_exact.p;
-        expand_device(ctx, recs(), a, wid, s);
+        return a;
+    }
+
+    // k_expand over jobs [b, e) of the planned sweep -> records sweep_first + [b, e)
+    void score_range(int64_t b, int64_t e) {
+        if (e <= b) return;
+        expand_device(ctx, recs(), sweep_args(b, e), wid, s);
+    }
+
+    // Multi-GPU sweep, one rank's share: the geometry (centre, normal,
+    // projection, colour, cell) of EVERY child of the sweep -- it depends only
+    // on parent records every rank holds -- and the photo test + accept test of
+    // the rank's own slice [b, e).  The other ranks then need only the slices'
+    // masks (mvs_stage_ingest -> ingest_masks).
+    void score_range_sharded(int64_t b, int64_t e) {
+        const ExpandArgs all = sweep_args(0, sweep_n);
+        if (sweep_n > 0 && mvs_launch_expand_geom(&ctx->sc, recs(), &all, s) != 0)
+            throw Fail{MVS_E_HIP, "expand_geom launch failed"};
+        if (e <= b) return;
+        const ExpandArgs a = sweep_args(b, e);
+        const int64_t f = a.first_out;
+        RecordsDev r = recs();
+        score_device(ctx, a.n, r.c + 3 * f, r.R + f, wid, a.thr, r.xy + 2 * f, r.mask + words * f,
+                     r.count + f, nullptr, s);
+        if (mvs_launch_expand_accept(r, &a, s) != 0) throw Fail{MVS_E_HIP, "expand_accept launch failed"};
+    }
+
+    // another rank's slice [b, e): its masks (words per child, from the
+    // all-gathered buffer) into the record table, then count and accept
+    void ingest_masks(int64_t b, int64_t e, const int64_t* d_masks) {
+        if (e <= b) return;
+        HIPCHK(hipMemcpyAsync(d_mask.p + (sweep_first + b) * words, d_masks, (e - b) * words * sizeof(uint64_t),
+                              hipMemcpyDeviceToDevice, s));
+        const ExpandArgs a = sweep_args(b, e);
+        if (mvs_launch_expand_ingest(recs(), &a, words, s) != 0) throw Fail{MVS_E_HIP, "expand_ingest launch failed"};
     }
 
     void fetch_sweep() { fetch_range(sweep_first, sweep_n); }
@@ -971,74 +1090,25 @@ struct Engine {
         HIPCHK(hipMemcpyAsync(hc.data(), d_c.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(hn.data(), d_n.p, nrec * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        // (key, event) entries, key = (v * nci + ci) * ncj + cj; events in fill order
-        std::vector<std::pair<int64_t, int32_t>> ent;
+        // the events' patches, in fill order
+        std::vector<int32_t> ecell(2 * nev), ecount(nev);
+        std::vector<uint64_t> emask(nev * words);
+        std::vector<double> ec(3 * nev), en(3 * nev);
         for (int64_t e = 0; e < nev; ++e) {
             const int64_t r = events[e];
-            const int cx = h_cell[2 * r], cy = h_cell[2 * r + 1];
-            if (cx < 0 || cx >= nci || cy < 0 || cy >= ncj) continue;
-            for (int w = 0; w < words; ++w)
-                for (uint64_t m = h_mask[r * words + w]; m; m &= m - 1) {
-                    const int v = 64 * w + __builtin_ctzll(m);
-                    ent.push_back({((int64_t)v * nci + cx) * ncj + cy, (int32_t)e});
-                }
+            ecell[2 * e] = h_cell[2 * r];
+            ecell[2 * e + 1] = h_cell[2 * r + 1];
+            ecount[e] = h_count[r];
+            for (int w = 0; w < words; ++w) emask[e * words + w] = h_mask[r * words + w];
+            for (int j = 0; j < 3; ++j) {
+                ec[3 * e + j] = hc[3 * r + j];
+                en[3 * e + j] = hn[3 * r + j];
+            }
         }
-        std::sort(ent.begin(), ent.end());
         std::vector<uint8_t> alive(nev, 1);
-        auto cnt = [&](int32_t e) { return h_count[events[e]]; };
-        // is_patch_neighbor(p1, p2, 0.2) (MVS2.py:298-299), numpy's 3-element dots
-        auto neighbor = [&](int32_t e1, int32_t e2) {
-            const double* c1 = &hc[3 * (int64_t)events[e1]];
-            const double* c2 = &hc[3 * (int64_t)events[e2]];
-            const double* n1 = &hn[3 * (int64_t)events[e1]];
-            const double* n2 = &hn[3 * (int64_t)events[e2]];
-            const double d0 = c1[0] - c2[0], d1 = c1[1] - c2[1], d2 = c1[2] - c2[2];
-            return std::fabs(fma_dot3(d0, d1, d2, n1[0], n1[1], n1[2]) + fma_dot3(d0, d1, d2, n2[0], n2[1], n2[2])) < 0.2;
-        };
-        std::vector<int32_t> L, out;
         int64_t removed = 0, lines = 0;
-        for (size_t b = 0; b < ent.size();) {
-            size_t e_end = b;
-            while (e_end < ent.size() && ent[e_end].first == ent[b].first) ++e_end;
-            L.clear();
-            double thr = 0.0;
-            int64_t len = 0;
-            for (size_t k = b; k < e_end; ++k) {
-                const int32_t e = ent[k].second;
-                if (!alive[e]) continue;
-                L.push_back(e);
-                const int m = cnt(e);
-                for (int i = 0; i < m; ++i) thr += 1.0 - avg[e];
-                len += m;
-            }
-            if (len == 0) {
-                const int64_t key = ent[b].first;
-                char msg[200];
-                std::snprintf(msg, sizeof msg,
-                              "filter_out_outlier: ZeroDivisionError (MVS2.py:144): every patch of filled cell "
-                              "(view %lld, %lld, %lld) was removed before it was visited",
-                              (long long)(key / ((int64_t)nci * ncj)), (long long)(key / ncj % nci),
-                              (long long)(key % ncj));
-                throw Fail{MVS_E_DIVZERO, msg};
-            }
-            thr /= (double)len;
-            out.clear();
-            for (int32_t p2 : L) {
-                if (!((double)cnt(p2) * avg[p2] < thr)) continue;
-                for (int32_t p1 : L)
-                    if (p1 != p2 && !neighbor(p1, p2)) {
-                        out.push_back(p2);
-                        break;
-                    }
-            }
-            for (int32_t p : out)
-                if (alive[p]) {
-                    alive[p] = 0;
-                    ++removed;
-                    lines += (int64_t)cnt(p) * cnt(p);
-                }
-            b = e_end;
-        }
+        filter_outliers_core(nev, words, nci, ncj, ecell.data(), emask.data(), ecount.data(), avg.data(),
+                             ec.data(), en.data(), alive.data(), &removed, &lines);
         std::vector<int32_t> kept;
         kept.reserve(nev - removed);
         for (int64_t e = 0; e < nev; ++e)
@@ -1303,6 +1373,35 @@ int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* 
     });
 }
 
+int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* cell, const uint64_t* mask,
+                        const int32_t* count, const double* avg, const double* c, const double* nrm,
+                        uint8_t* alive, int64_t* stats) {
+    if (n < 0 || words < 1 || nci < 1 || ncj < 1 || !stats ||
+        (n > 0 && (!cell || !mask || !count || !avg || !c || !nrm || !alive)))
+        return set_err(nullptr, Fail{MVS_E_ARG, "bad arguments"});
+    return guarded(nullptr, [&]() {
+        filter_outliers_core(n, words, nci, ncj, cell, mask, count, avg, c, nrm, alive, &stats[0], &stats[1]);
+        return 0;
+    });
+}
+
+int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count, const uint64_t* d_mask,
+                      const double* d_c, int vlb, int64_t cap, int64_t* d_out, void* stream) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (n < 0 || cap < 0 || !d_out || (n > 0 && (!d_count || !d_mask || !d_c)))
+        return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
+    return guarded(ctx, [&]() {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        ctx->scratch_acquire(s);
+        ctx->p_chunk.ensure(std::max<int64_t>((n + 1023) / 1024, 1));
+        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, ctx->words(), d_c, vlb, cap, ctx->p_chunk.p,
+                                     d_out, s) != 0)
+            throw Fail{MVS_E_HIP, "pack launch failed"};
+        ctx->scratch_release(s);
+        return 0;
+    });
+}
+
 int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int wid, double min_ncc,
               double* xy, uint64_t* mask, int32_t* count, double* avg) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
@@ -1431,7 +1530,7 @@ int64_t mvs_stage_plan(mvs_stage* st) {
 
 int mvs_stage_record_width(const mvs_stage* st) {
     if (!st) return MVS_E_ARG;
-    return 8 + st->E->words + 3;
+    return st->E->words;
 }
 
 int mvs_stage_score_slice(mvs_stage* st, int64_t* d_out) {
@@ -1440,12 +1539,17 @@ int mvs_stage_score_slice(mvs_stage* st, int64_t* d_out) {
     if (st->world > 1 && !d_out) return set_err(st->ctx, Fail{MVS_E_ARG, "null slice buffer"});
     const int rc = guarded(st->ctx, [&]() {
         Engine* E = st->E.get();
-        int64_t b, e;
-        Engine::shard(E->sweep_n, st->rank, st->world, &b, &e);
-        E->score_range(b, e);
-        if (st->world > 1 &&
-            mvs_launch_pack_records(E->recs(), E->words, E->sweep_first + b, e - b, d_out, E->s) != 0)
-            throw Fail{MVS_E_HIP, "pack launch failed"};
+        if (st->world == 1) {
+            E->score_range(0, E->sweep_n);
+        } else {
+            int64_t b, e;
+            Engine::shard(E->sweep_n, st->rank, st->world, &b, &e);
+            E->score_range_sharded(b, e);
+            // the slice's exchange record is its mask words: contiguous in the table
+            if (e > b)
+                HIPCHK(hipMemcpyAsync(d_out, E->d_mask.p + (E->sweep_first + b) * E->words,
+                                      (e - b) * E->words * sizeof(uint64_t), hipMemcpyDeviceToDevice, E->s));
+        }
         HIPCHK(hipStreamSynchronize(E->s));
         return 0;
     });
@@ -1461,14 +1565,12 @@ int mvs_stage_ingest(mvs_stage* st, const int64_t* d_all) {
         Engine* E = st->E.get();
         if (st->world > 1) {
             const int64_t smax = (E->sweep_n + st->world - 1) / st->world;
-            const int64_t w = 8 + E->words + 3;
+            const int64_t w = E->words;
             for (int r = 0; r < st->world; ++r) {
                 if (r == st->rank) continue;   // own slice is already in the record table
                 int64_t b, e;
                 Engine::shard(E->sweep_n, r, st->world, &b, &e);
-                if (mvs_launch_unpack_records(E->recs(), E->words, E->sweep_first + b, e - b,
-                                              d_all + (int64_t)r * smax * w, E->s) != 0)
-                    throw Fail{MVS_E_HIP, "unpack launch failed"};
+                E->ingest_masks(b, e, d_all + (int64_t)r * smax * w);
             }
         }
         E->fetch_sweep();

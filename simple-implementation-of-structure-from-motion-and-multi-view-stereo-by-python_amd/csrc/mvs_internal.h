@@ -155,12 +155,16 @@ int mvs_launch_expand(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, i
 // the accept test from the scored counts
 int mvs_launch_expand_geom(const SceneDev* sc, RecordsDev rec, const ExpandArgs* a, hipStream_t s);
 int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hipStream_t s);
-// Packed record rows for the multi-GPU stage exchange: int64 words
-// [c0 c1 c2 n0 n1 n2 x y | mask[words] | R + count<<32 | cell0 + cell1<<32 | rgba + accept<<32]
-int mvs_launch_pack_records(RecordsDev rec, int words, int64_t first, int64_t n, int64_t* out,
-                            hipStream_t s);
-int mvs_launch_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n,
-                              const int64_t* in, hipStream_t s);
+// Multi-GPU stage, ingest side: count = popcount(mask) and the accept test
+// of children whose masks another rank scored (geometry already in place)
+int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hipStream_t s);
+// The accepted candidates of a sweep slice as exchange rows [global index,
+// mask words, x y z bits] after a header row [accepted, n, cap, 0...], in
+// index order, at most cap rows (parallel.PointsExchange); chunk_acc holds
+// ceil(n / 1024) int32
+int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, int words,
+                             const double* c, int vlb, int64_t cap, int32_t* chunk_acc, int64_t* out,
+                             hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
                            int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
 // stage output order on the device (reconstruct_from_Q, MVS2.py:159-173):

@@ -1713,41 +1713,100 @@ __global__ void k_ncc_windows(int64_t n, int npx, const uint8_t* __restrict__ A,
     }
 }
 
-__global__ void k_pack_records(RecordsDev rec, int words, int64_t first, int64_t n, int64_t* out) {
-    const int w = 8 + words + 3;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+// Sharded sweep, ingest side: every rank computed the whole sweep's child
+// geometry (k_expand_geom) and received the other ranks' photo-test masks,
+// so a child's count (|V| = popcount of its mask, MVS2.py:72-74) and its
+// accept test (MVS2.py:369) follow here.
+__global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.n;
          k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = first + k;
-        int64_t* o = out + k * w;
-        for (int q = 0; q < 3; ++q) o[q] = __double_as_longlong(rec.c[3 * r + q]);
-        for (int q = 0; q < 3; ++q) o[3 + q] = __double_as_longlong(rec.n[3 * r + q]);
-        o[6] = __double_as_longlong(rec.xy[2 * r]);
-        o[7] = __double_as_longlong(rec.xy[2 * r + 1]);
-        for (int q = 0; q < words; ++q) o[8 + q] = (int64_t)rec.mask[r * words + q];
-        o[8 + words] = (int64_t)(uint32_t)rec.R[r] | ((int64_t)(uint32_t)rec.count[r] << 32);
-        o[9 + words] = (int64_t)(uint32_t)rec.cell[2 * r] | ((int64_t)(uint32_t)rec.cell[2 * r + 1] << 32);
-        const uint32_t rgba = *(const uint32_t*)(rec.color + 4 * r);
-        o[10 + words] = (int64_t)rgba | ((int64_t)rec.accept[r] << 32);
+        const ChildJob job = a.jobs[k];
+        const int64_t out = a.first_out + k;
+        int cnt = 0;
+        for (int q = 0; q < words; ++q) cnt += __popcll(rec.mask[out * words + q]);
+        rec.count[out] = cnt;
+        const double X[3] = {rec.c[3 * out], rec.c[3 * out + 1], rec.c[3 * out + 2]};
+        const double nX[3] = {rec.n[3 * out], rec.n[3 * out + 1], rec.n[3 * out + 2]};
+        rec.accept[out] = child_accept(rec, a, job.parent, X, nX, cnt);
     }
 }
 
-__global__ void k_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n, const int64_t* in) {
-    const int w = 8 + words + 3;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = first + k;
-        const int64_t* o = in + k * w;
-        for (int q = 0; q < 3; ++q) rec.c[3 * r + q] = __longlong_as_double(o[q]);
-        for (int q = 0; q < 3; ++q) rec.n[3 * r + q] = __longlong_as_double(o[3 + q]);
-        rec.xy[2 * r] = __longlong_as_double(o[6]);
-        rec.xy[2 * r + 1] = __longlong_as_double(o[7]);
-        for (int q = 0; q < words; ++q) rec.mask[r * words + q] = (uint64_t)o[8 + q];
-        rec.R[r] = (int32_t)(uint32_t)o[8 + words];
-        rec.count[r] = (int32_t)(uint32_t)((uint64_t)o[8 + words] >> 32);
-        rec.cell[2 * r] = (int32_t)(uint32_t)o[9 + words];
-        rec.cell[2 * r + 1] = (int32_t)(uint32_t)((uint64_t)o[9 + words] >> 32);
-        *(uint32_t*)(rec.color + 4 * r) = (uint32_t)o[10 + words];
-        rec.accept[r] = (uint8_t)((uint64_t)o[10 + words] >> 32);
+// ---------------------------------------------------------------------------
+// The multi-GPU sweep's exchange record set (parallel.PointsExchange): the
+// accepted candidates of a rank's slice (|V| >= vlb, MVS2.py:256/369) packed
+// in index order into rows [global index, mask words..., x, y, z bits] of a
+// fixed-capacity buffer whose row 0 is the header [accepted, n, cap, 0, ...].
+// No host synchronisation: the accepted total travels in the header, and a
+// slice with more than cap accepted candidates keeps its first cap rows (the
+// receiver sees accepted > cap).  Two launches: per-chunk accepted counts,
+// then each chunk's rows at (sum of the earlier chunks' counts) + its rank.
+// ---------------------------------------------------------------------------
+constexpr int kAccChunk = 1024;
+
+__global__ __launch_bounds__(kAccChunk) void k_acc_count(int64_t n, const int32_t* __restrict__ count, int vlb,
+                                                          int32_t* __restrict__ chunk_acc) {
+    __shared__ int32_t wt[kAccChunk / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t b = blockIdx.x; b * kAccChunk < n; b += gridDim.x) {
+        const int64_t i = b * kAccChunk + threadIdx.x;
+        const uint64_t m = __ballot(i < n && count[i] >= vlb);
+        if (lane == 0) wt[wave] = __popcll(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int w = 0; w < kAccChunk / 64; ++w) t += wt[w];
+            chunk_acc[b] = t;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kAccChunk) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
+                                                         const uint64_t* __restrict__ mask, int words,
+                                                         const double* __restrict__ c, int vlb, int64_t cap,
+                                                         const int32_t* __restrict__ chunk_acc, int64_t* __restrict__ out) {
+    __shared__ int32_t wt[kAccChunk / 64];
+    __shared__ int32_t red[kAccChunk / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int width = 1 + words + 3;
+    const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
+    // an empty slice still has chunk 0, which writes the header
+    for (int64_t b = blockIdx.x; b < (nchunk > 0 ? nchunk : 1); b += gridDim.x) {
+        // rows before this chunk: the earlier chunks' counts (chunk 0 also
+        // sums them all for the header)
+        const int64_t lim = b == 0 ? nchunk : b;
+        int64_t part = 0;
+        for (int64_t k = threadIdx.x; k < lim; k += kAccChunk) part += chunk_acc[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+        if (lane == 0) red[wave] = (int32_t)part;
+        const int64_t i = b * kAccChunk + threadIdx.x;
+        const bool acc = i < n && count[i] >= vlb;
+        const uint64_t m = __ballot(acc);
+        if (lane == 0) wt[wave] = __popcll(m);
+        __syncthreads();
+        int64_t base = 0, wbase = 0;
+        for (int w = 0; w < kAccChunk / 64; ++w) {
+            base += red[w];
+            wbase += w < wave ? wt[w] : 0;
+        }
+        if (b == 0) {
+            if (threadIdx.x == 0) {
+                out[0] = base;             // accepted in the whole slice
+                out[1] = n;
+                out[2] = cap;
+                for (int q = 3; q < width; ++q) out[q] = 0;
+            }
+            base = 0;
+        }
+        const int64_t pos = base + wbase + __popcll(m & ((1ull << lane) - 1ull));
+        if (acc && pos < cap) {
+            int64_t* o = out + (1 + pos) * width;
+            o[0] = offset + i;
+            for (int q = 0; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
+            for (int q = 0; q < 3; ++q) o[1 + words + q] = __double_as_longlong(c[3 * i + q]);
+        }
+        __syncthreads();
     }
 }
 
@@ -2060,20 +2119,23 @@ extern "C" int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hip
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mvs_launch_pack_records(RecordsDev rec, int words, int64_t first, int64_t n,
-                                       int64_t* out, hipStream_t s) {
-    if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_pack_records, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, rec, words, first, n, out);
+extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask,
+                                        int words, const double* c, int vlb, int64_t cap, int32_t* chunk_acc,
+                                        int64_t* out, hipStream_t s) {
+    const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, 2048));
+    if (n > 0) hipLaunchKernelGGL(k_acc_count, dim3(grid), dim3(kAccChunk), 0, s, n, count, vlb, chunk_acc);
+    // n == 0 still writes the header (chunk 0 of an empty slice)
+    hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccChunk), 0, s, n, offset, count, mask, words, c, vlb, cap,
+                       chunk_acc, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mvs_launch_unpack_records(RecordsDev rec, int words, int64_t first, int64_t n,
-                                         const int64_t* in, hipStream_t s) {
-    if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_unpack_records, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, rec, words, first, n, in);
+extern "C" int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hipStream_t s) {
+    if (a->n <= 0) return 0;
+    hipLaunchKernelGGL(k_expand_ingest, dim3(grid_for(a->n, 256, 4096)), dim3(256), 0, s, rec, *a, words);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-
 extern "C" int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b,
                                       double thr, int force_exact, double* ncc, uint8_t* pass,
                                       hipStream_t s) {

@@ -1,22 +1,21 @@
-"""Multi-GPU sweeps: candidate batches sharded over ranks, accepted records
+"""Multi-GPU sweeps: candidate batches sharded over ranks, accepted points
 all-gathered (RCCL over xGMI on MI355X, gloo on CPU for tests).
 
 One process per GPU (torch.distributed, backend "nccl" == RCCL on ROCm).
 Every candidate's photo test depends only on read-only data (images,
 cameras), so a sweep's candidates split into contiguous per-rank slices with
-no communication while scoring.  The only exchange is at the end of the
-sweep: each rank packs the candidates it accepted (|V| >= vlb,
-MVS2.py:256/369) as fixed-width int64 records and all-gathers them, so every
-rank holds the sweep's accepted set -- the input of the replicated,
-order-deterministic commit.
+no communication while scoring.  Two exchanges:
 
-Record layout (int64 columns): [global index, count, mask words..., x bits, y bits].
-
-stage_sharded() runs the whole DensePointsWithMVS2 stage this way: every
-expansion sweep (the children of a block of queued patches, MVS2.py:329-369)
-is split into contiguous per-rank slices, each rank scores its slice on its
-GPU, the packed records are all-gathered, and every rank runs the identical
-ordered commit (mvs_stage_* in include/mvs_amd.h).
+* PointsExchange -- the bench's per-sweep exchange: each rank's accepted
+  candidates (|V| >= vlb, MVS2.py:256/369) as rows [global index, mask
+  words, x y z] packed on the device (mvs_pack_accepted, no host sync) into
+  a fixed-capacity buffer and all-gathered on a communication stream while
+  the next sweep scores (double-buffered).
+* stage_sharded -- the whole DensePointsWithMVS2 stage: every rank computes
+  the geometry of every child of a sweep (it depends only on records every
+  rank holds), scores its contiguous slice, and the slices' photo-test masks
+  (8 B per child at V <= 64) are all-gathered; every rank then runs the
+  identical ordered commit (mvs_stage_* in include/mvs_amd.h).
 """
 import torch
 import torch.distributed as dist
@@ -29,206 +28,112 @@ def shard_range(n, rank, world):
     return begin, begin + base + (1 if rank < extra else 0)
 
 
-def record_width(words):
-    return 2 + words + 2
+def points_width(words):
+    """int64 columns of an exchange row: global index, mask words, x y z bits."""
+    return 1 + words + 3
 
 
-def pack_accepted(offset, count, mask, xy, vlb):
-    """Accepted candidates of this rank's slice as int64 records (k, record_width)."""
-    acc = torch.nonzero(count >= vlb).squeeze(1)
+def pack_accepted_reference(offset, count, mask, c, vlb, out):
+    """mvs_pack_accepted's layout from torch ops, for CPU tensors only (the
+    gloo process groups of the CPU tests): header [accepted, n, cap, 0...],
+    then up to cap rows in index order.  Device tensors never come here."""
+    if count.is_cuda:
+        raise RuntimeError("pack_accepted_reference is for CPU tensors; device slices use mvs_pack_accepted")
+    cap = out.shape[0] - 1
     words = mask.shape[1]
-    rec = torch.empty((acc.numel(), record_width(words)), dtype=torch.int64, device=count.device)
-    if acc.numel():
-        rec[:, 0] = acc + offset
-        rec[:, 1] = count[acc].to(torch.int64)
-        rec[:, 2:2 + words] = mask[acc].view(torch.int64)
-        rec[:, 2 + words:] = xy[acc].contiguous().view(torch.int64)
-    return rec
+    idx = torch.nonzero(count >= vlb).squeeze(1)
+    out.zero_()
+    out[0, 0] = idx.numel()
+    out[0, 1] = count.numel()
+    out[0, 2] = cap
+    idx = idx[:cap]
+    k = idx.numel()
+    out[1:1 + k, 0] = idx + offset
+    out[1:1 + k, 1:1 + words] = mask[idx].view(torch.int64)
+    out[1:1 + k, 1 + words:] = c[idx].contiguous().view(torch.int64)
 
 
-def all_gather_records(rec, group=None):
-    """All-gather variable-length record blocks; returns them concatenated in rank order."""
-    world = dist.get_world_size(group)
-    if world == 1:
-        return rec
-    k = torch.tensor([rec.shape[0]], dtype=torch.int64, device=rec.device)
-    ks = [torch.empty_like(k) for _ in range(world)]
-    dist.all_gather(ks, k, group=group)
-    sizes = [int(x.item()) for x in ks]
-    kmax = max(max(sizes), 1)
-    buf = torch.zeros((kmax, rec.shape[1]), dtype=rec.dtype, device=rec.device)
-    buf[:rec.shape[0]] = rec
-    outs = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(outs, buf, group=group)
-    return torch.cat([o[:s] for o, s in zip(outs, sizes)], 0)
+class PointsExchange:
+    """Per-sweep all-gather of the accepted 3D points,
+    pipelined: post() packs this rank's accepted rows on the scoring stream
+    (no host sync) and starts the all-gather on a communication stream that
+    waits only for that pack, so the next sweep scores while it runs.  The
+    two send / receive buffers alternate; a pack waits for the all-gather that
+    used its buffer two sweeps before.  cap = rows per rank (the bench takes
+    the first sweep's accepted count plus a margin); a rank with more than cap
+    accepted candidates shows it in its header (check() raises).
 
+    ctx = the rank's MvsContext (its pack kernel); on CPU tensors (gloo) the
+    torch reference pack is used and the all-gather is synchronous."""
 
-def unpack_records(rec, words):
-    """-> (index, count, mask (k, words) uint64 view as int64, xy (k, 2) float64)."""
-    idx = rec[:, 0]
-    count = rec[:, 1].to(torch.int32)
-    mask = rec[:, 2:2 + words]
-    xy = rec[:, 2 + words:].contiguous().view(torch.float64)
-    return idx, count, mask, xy
+    def __init__(self, ctx, words, cap, device, group=None):
+        self.ctx, self.words, self.cap, self.group = ctx, words, int(cap), group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.width = points_width(words)
+        self.device = torch.device(device)
+        cuda = self.device.type == "cuda"
+        self.send = [torch.zeros((self.cap + 1, self.width), dtype=torch.int64, device=device) for _ in range(2)]
+        self.recv = [torch.zeros((self.world * (self.cap + 1), self.width), dtype=torch.int64, device=device)
+                     for _ in range(2)]
+        self.comm = torch.cuda.Stream(self.device) if cuda and self.world > 1 else None
+        self.done = [None, None]
+        self.posted = 0
 
+    def post(self, offset, count, mask, c, vlb, stream=None):
+        """Pack this rank's accepted rows of a scored slice and start the
+        all-gather; returns the buffer index for result()."""
+        b = self.posted & 1
+        self.posted += 1
+        if count.is_cuda:
+            cur = stream if stream is not None else torch.cuda.current_stream(self.device)
+            if self.done[b] is not None:
+                cur.wait_event(self.done[b])          # the all-gather two sweeps back has read send[b]
+            self.ctx.pack_accepted(offset, count, mask, c, vlb, self.send[b], stream=cur.cuda_stream)
+            if self.world == 1:
+                return b
+            packed = torch.cuda.Event()
+            packed.record(cur)
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(packed)
+                work = dist.all_gather_into_tensor(self.recv[b], self.send[b], group=self.group, async_op=True)
+                work.wait()                           # the comm stream (not the host) waits for RCCL
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+            self.done[b] = ev
+            return b
+        pack_accepted_reference(offset, count, mask, c, vlb, self.send[b])
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.recv[b], self.send[b], group=self.group)
+        return b
 
-# Compact form of a rank's accepted set (the bench's per-sweep exchange): one
-# int64 block [k, accept bitmap (ceil(n/64) words, bit i = candidate i),
-# masks of the k accepted candidates (k*words)].  count = popcount(mask) and
-# the candidates' centroids / projections are known to every rank (the
-# sweep's candidate list is), so the bitmap and the masks are the whole
-# accepted set at 8 B per accepted candidate plus n/8 B -- 5x less than the
-# explicit records above, which matters on xGMI at N = 8.
-def pack_compact(count, mask, vlb):
-    n = count.numel()
-    words = mask.shape[1]
-    nbw = (n + 63) // 64
-    acc = count >= vlb
-    a = acc.to(torch.int64)
-    if nbw * 64 != n:
-        a = torch.cat([a, a.new_zeros(nbw * 64 - n)])
-    sh = torch.arange(64, dtype=torch.int64, device=count.device)
-    bits = (a.view(nbw, 64) << sh).sum(1)            # distinct bits: the sum is their OR
-    masks = mask[acc].reshape(-1)
-    k = masks.numel() // max(words, 1)
-    head = torch.full((1,), k, dtype=torch.int64, device=count.device)
-    return torch.cat([head, bits, masks.view(torch.int64)])
+    def blocks(self, b):
+        """(world, cap + 1, width) view of buffer b's gathered rows (device);
+        the caller orders its stream after the gather (wait_done)."""
+        src = self.recv[b] if self.world > 1 else self.send[b]
+        return src.view(self.world, self.cap + 1, self.width)
 
+    def wait_done(self, b, stream=None):
+        if self.done[b] is not None:
+            (stream or torch.cuda.current_stream(self.device)).wait_event(self.done[b])
 
-def all_gather_compact(block, group=None):
-    """All-gather the ranks' compact blocks -> list of blocks in rank order."""
-    world = dist.get_world_size(group)
-    if world == 1:
-        return [block]
-    k = torch.tensor([block.numel()], dtype=torch.int64, device=block.device)
-    ks = torch.empty(world, dtype=torch.int64, device=block.device)
-    dist.all_gather_into_tensor(ks, k, group=group)
-    sizes = ks.tolist()
-    kmax = max(sizes)
-    buf = torch.zeros(kmax, dtype=torch.int64, device=block.device)
-    buf[:block.numel()] = block
-    flat = torch.empty(world * kmax, dtype=torch.int64, device=block.device)
-    dist.all_gather_into_tensor(flat, buf, group=group)
-    return [flat[r * kmax: r * kmax + sizes[r]] for r in range(world)]
+    def result(self, b):
+        """The gathered accepted rows of every rank, concatenated in rank order
+        (host sync; a consumer of the exchange, not the timed loop):
+        (global index, mask (k, words) int64 view, points (k, 3) float64)."""
+        if self.done[b] is not None:
+            self.done[b].synchronize()
+        blk = self.blocks(b)
+        self.check(blk)
+        rows = torch.cat([blk[r, 1:1 + int(blk[r, 0, 0])] for r in range(blk.shape[0])])
+        return rows[:, 0], rows[:, 1:1 + self.words], rows[:, 1 + self.words:].contiguous().view(torch.float64)
 
-
-def exchange_accepted(count, mask, vlb, group=None):
-    """pack_compact + all_gather_compact with ONE host synchronisation: the
-    accepted counts travel first (a tiny all-gather), their host copy sizes
-    both the static-size compaction (nonzero_static, no sync of its own) and
-    the padded data all-gather.  Returns the ranks' compact blocks."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    n = count.numel()
-    words = mask.shape[1]
-    nbw = (n + 63) // 64
-    acc = count >= vlb
-    k = acc.sum().to(torch.int64).reshape(1)
-    if world > 1:
-        ks = torch.empty(world, dtype=torch.int64, device=count.device)
-        dist.all_gather_into_tensor(ks, k, group=group)
-    else:
-        ks = k
-    a = acc.to(torch.int64)
-    if nbw * 64 != n:
-        a = torch.cat([a, a.new_zeros(nbw * 64 - n)])
-    sh = torch.arange(64, dtype=torch.int64, device=count.device)
-    bits = (a.view(nbw, 64) << sh).sum(1)
-    sizes = ks.tolist()                               # the one host sync
-    rank = dist.get_rank(group) if world > 1 else 0
-    kmax = max(sizes)
-    buf = torch.zeros(1 + nbw + kmax * words, dtype=torch.int64, device=count.device)
-    buf[0] = k[0]
-    buf[1:1 + nbw] = bits
-    if sizes[rank]:
-        idx = torch.nonzero_static(acc, size=sizes[rank]).squeeze(1)
-        buf[1 + nbw:1 + nbw + sizes[rank] * words] = mask[idx].reshape(-1).view(torch.int64)
-    if world == 1:
-        return [buf[:1 + nbw + sizes[0] * words]]
-    flat = torch.empty(world * buf.numel(), dtype=torch.int64, device=count.device)
-    dist.all_gather_into_tensor(flat, buf, group=group)
-    L = buf.numel()
-    return [flat[r * L: r * L + 1 + nbw + sizes[r] * words] for r in range(world)]
-
-
-def exchange_accepted_points(offset, count, mask, c, vlb, group=None):
-    """The sweep's exchange step: every rank's accepted
-    candidates (|V| >= vlb, MVS2.py:256/369) as int64 records
-    [global index, count, mask words..., x, y, z (float64 bits)] -- the 3D
-    points included -- all-gathered over the group (RCCL over xGMI for the
-    nccl backend) with one host synchronisation (the record counts travel
-    first).  offset = global index of this rank's candidate 0.
-    Returns the records of all ranks, concatenated in rank order."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    words = mask.shape[1]
-    width = 2 + words + 3
-    acc = count >= vlb
-    k = acc.sum().to(torch.int64).reshape(1)
-    if world > 1:
-        ks = torch.empty(world, dtype=torch.int64, device=count.device)
-        dist.all_gather_into_tensor(ks, k, group=group)
-    else:
-        ks = k
-    sizes = ks.tolist()                               # the one host sync
-    rank = dist.get_rank(group) if world > 1 else 0
-    kmax = max(max(sizes), 1)
-    buf = torch.zeros((kmax, width), dtype=torch.int64, device=count.device)
-    if sizes[rank]:
-        idx = torch.nonzero_static(acc, size=sizes[rank]).squeeze(1)
-        buf[:sizes[rank], 0] = idx + offset
-        buf[:sizes[rank], 1] = count[idx].to(torch.int64)
-        buf[:sizes[rank], 2:2 + words] = mask[idx].view(torch.int64)
-        buf[:sizes[rank], 2 + words:] = c[idx].contiguous().view(torch.int64)
-    if world == 1:
-        return buf[:sizes[0]]
-    flat = torch.empty((world * kmax, width), dtype=torch.int64, device=count.device)
-    dist.all_gather_into_tensor(flat, buf, group=group)
-    return torch.cat([flat[r * kmax: r * kmax + sizes[r]] for r in range(world)])
-
-
-def unpack_points(rec, words):
-    """-> (global index, count, mask (k, words) int64 view, points (k, 3) float64)."""
-    return rec[:, 0], rec[:, 1].to(torch.int32), rec[:, 2:2 + words], \
-        rec[:, 2 + words:].contiguous().view(torch.float64)
-
-
-_POP8 = None
-
-
-def unpack_compact(blocks, n, words):
-    """Compact blocks of ranks 0..world-1 (slices of n candidates each, rank r's
-    candidate i = global index r*n + i) -> (index, count, mask) in global order."""
-    global _POP8
-    idx, cnt, msk = [], [], []
-    nbw = (n + 63) // 64
-    for r, b in enumerate(blocks):
-        k = int(b[0].item())
-        bits = b[1:1 + nbw]
-        sh = torch.arange(64, dtype=torch.int64, device=b.device)
-        flags = ((bits.unsqueeze(1) >> sh) & 1).reshape(-1)[:n].bool()
-        ii = torch.nonzero(flags).squeeze(1) + r * n
-        m = b[1 + nbw:1 + nbw + k * words].reshape(k, words)
-        if _POP8 is None or _POP8.device != b.device:
-            _POP8 = torch.tensor([bin(v).count("1") for v in range(256)], dtype=torch.int32,
-                                 device=b.device)
-        c = _POP8[m.contiguous().view(torch.uint8).long()].reshape(k, -1).sum(1).to(torch.int32)
-        idx.append(ii)
-        cnt.append(c)
-        msk.append(m)
-    return torch.cat(idx), torch.cat(cnt), torch.cat(msk)
-
-
-def sharded_sweep(score_fn, c, ref, vlb, words, group=None):
-    """Score the sweep [c, ref] (all ranks pass the same full batch) by slices and
-    exchange the accepted records.  score_fn(c_slice, ref_slice) -> (xy, mask, count)
-    as tensors.  Returns (index, count, mask, xy) of every accepted candidate of the
-    sweep, in global index order, identical on every rank."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    b, e = shard_range(len(ref), rank, world)
-    xy, mask, count = score_fn(c[b:e], ref[b:e])
-    rec = pack_accepted(b, count, mask, xy, vlb)
-    allrec = all_gather_records(rec, group) if world > 1 else rec
-    return unpack_records(allrec, words)
+    def check(self, blk=None):
+        """Raise if any rank accepted more candidates than the capacity."""
+        blk = self.blocks((self.posted - 1) & 1) if blk is None else blk
+        acc = blk[:, 0, 0].tolist()
+        if max(acc) > self.cap:
+            raise RuntimeError(f"PointsExchange capacity {self.cap} < accepted {max(acc)}")
+        return acc
 
 
 def gather_slices(out, group=None):

@@ -16,6 +16,9 @@ Outputs (all data, no reference source):
                         out: reconstruct_from_Q (called right after, MVS2.py:285) is
                         wrapped to run the filter first; also the number of
                         "remove a outlier" lines it printed
+  filter_crafted.npz    filter_out_outlier on crafted patch sets (stub patches
+                        with random avg / normals / V lists) where it removes
+                        patches or raises ZeroDivisionError
 """
 import argparse
 import contextlib
@@ -226,12 +229,82 @@ def stage_golden(MVS2, imgs, tracks, cap, with_filter=False):
     return out
 
 
+def filter_crafted_golden(MVS2, n_cases=60, seed=2024):
+    """filter_out_outlier (MVS2.py:132-158) on crafted patch sets, where it
+    does remove patches (with the stage's own parameters it provably cannot,
+    DESIGN 4.3): stub MyPatch objects (MVS2.py:45-57) with random centres,
+    normals, avg_ncc_score and V lists (every entry at the patch's own x, y,
+    as the photo test produces them, MVS2.py:68/74) are filled into a CellTable
+    (MVS2.py:401-403: fill_with_point per V entry), then the reference's
+    filter runs and reconstruct_from_Q (MVS2.py:159-173) gives the survivors'
+    order.  Per case: the inputs in fill order, the survivor ids in output
+    order, the "remove a outlier" line count, and whether the filter raised
+    ZeroDivisionError (a filled cell emptied before its visit, MVS2.py:144)."""
+    rng = np.random.default_rng(seed)
+    H = W = 13                     # cell grid ceil(12/2) = 6 x 6 per view at cell size 2
+    cs = 2
+    out = {"cs": np.int64(cs), "H": np.int64(H), "W": np.int64(W)}
+    for k in range(n_cases):
+        V = int(rng.integers(2, 7))
+        npatch = int(rng.integers(2, 40))
+        ncell = int(rng.integers(1, 5))            # few cells: patches collide in them
+        cells = rng.integers(0, 6, (ncell, 2))
+        spread = float(rng.choice([0.05, 0.2, 0.5]))
+        imgs = [np.zeros((H, W), np.uint8) for _ in range(V)]
+        table = MVS2.CellTable(imgs, cell_size=cs)
+        pid, pview, pxy, pc, pn, pavg = [], [], [], [], [], []
+        patches = []
+        for p in range(npatch):
+            ci, cj = cells[rng.integers(0, ncell)]
+            x = cs * ci + rng.uniform(0, cs - 1e-6)
+            y = cs * cj + rng.uniform(0, cs - 1e-6)
+            nv = int(rng.integers(1, V + 1))
+            views = np.sort(rng.choice(V, nv, replace=False))
+            c = rng.normal(0, spread, 3)
+            nrm = rng.normal(0, 1, 3)
+            nrm /= np.linalg.norm(nrm)
+            obj = MVS2.MyPatch(c, nrm, int(views[0]), [[int(v), x, y] for v in views], np.array([p, 0, 0]), None)
+            obj.avg_ncc_score = float(rng.uniform(0.05, 0.95))
+            patches.append(obj)
+            mask = 0
+            for v in views:
+                mask |= 1 << int(v)
+            pid.append(p); pview.append(mask); pxy.append((x, y)); pc.append(c); pn.append(nrm)
+            pavg.append(obj.avg_ncc_score)
+            for h in obj.V:
+                table.fill_with_point(h[0], h[1], h[2], obj)
+        buf = io.StringIO()
+        divzero = False
+        try:
+            with contextlib.redirect_stdout(buf):
+                table.filter_out_outlier()
+        except ZeroDivisionError:
+            divzero = True
+        lines = buf.getvalue().count("remove a outlier")
+        surv = []
+        if not divzero:
+            pts, cols = table.reconstruct_from_Q()
+            surv = [int(col[0]) for col in cols]
+        out[f"c{k}_V"] = np.int64(V)
+        out[f"c{k}_mask"] = np.array(pview, np.uint64)
+        out[f"c{k}_xy"] = np.array(pxy, np.float64)
+        out[f"c{k}_c"] = np.array(pc, np.float64)
+        out[f"c{k}_n"] = np.array(pn, np.float64)
+        out[f"c{k}_avg"] = np.array(pavg, np.float64)
+        out[f"c{k}_survivors"] = np.array(surv, np.int64)
+        out[f"c{k}_lines"] = np.int64(lines)
+        out[f"c{k}_divzero"] = np.bool_(divzero)
+    out["n_cases"] = np.int64(n_cases)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--func", action="store_true")
     ap.add_argument("--seeds", action="store_true")
     ap.add_argument("--stage", type=int, nargs="*", default=[])
     ap.add_argument("--filter-stage", type=int, nargs="*", default=[])
+    ap.add_argument("--filter-crafted", action="store_true")
     a = ap.parse_args()
     assert os.path.isdir(REF), "the reference is only present in the build container"
     imgs, K, Rm, t = load_dino(DATA)
@@ -246,6 +319,12 @@ def main():
         out = func_golden(MVS2, imgs, K, Rm, t, rng)
         np.savez_compressed(os.path.join(HERE, "func_golden.npz"), **out)
         print("func golden written", {k: v.shape for k, v in out.items()})
+    if a.filter_crafted:
+        out = filter_crafted_golden(MVS2)
+        np.savez_compressed(os.path.join(HERE, "filter_crafted.npz"), **out)
+        nrem = sum(int(out[f"c{k}_lines"]) > 0 for k in range(int(out["n_cases"])))
+        ndz = sum(bool(out[f"c{k}_divzero"]) for k in range(int(out["n_cases"])))
+        print(f"filter_crafted: {int(out['n_cases'])} cases, {nrem} with removals, {ndz} ZeroDivisionError")
     for cap in a.stage:
         out = stage_golden(MVS2, imgs, seeds_to_tracks(seeds), cap)
         np.savez_compressed(os.path.join(HERE, f"stage_cap{cap}.npz"), **out)

@@ -98,3 +98,19 @@ def make_seeds(imgs, K, R, t, per_pair=30, max_try=1500, wid=5):
     obs_xy += np.random.default_rng(1).uniform(-0.25, 0.25, obs_xy.shape)
     return {"track_off": np.array(off, np.int64), "obs_view": np.array(obs_v, np.int32),
             "obs_xy": obs_xy.astype(np.float32)}
+
+
+def subset_seeds(seeds, n_views):
+    """The tracks whose every observation lies in views 0..n_views-1 (the
+    47-view dinoRing subset standing in for BASELINE config 3's 47 views;
+    templeRing itself is absent)."""
+    off, ov, oxy = seeds["track_off"], seeds["obs_view"], seeds["obs_xy"]
+    keep_off, keep_v, keep_xy = [0], [], []
+    for k in range(len(off) - 1):
+        v = ov[off[k]:off[k + 1]]
+        if (v < n_views).all():
+            keep_v += list(v)
+            keep_xy += list(oxy[off[k]:off[k + 1]])
+            keep_off.append(len(keep_v))
+    return (np.array(keep_off, np.int64), np.array(keep_v, np.int32),
+            np.array(keep_xy, np.float32).reshape(-1, 2))

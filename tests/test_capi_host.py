@@ -67,3 +67,42 @@ def test_ply_roundtrip(pkg, tmp_path):
     pkg.export2ply(pts, col, path=p)
     back = pkg.read_ply(p + ".ply")
     assert np.array_equal(back, np.hstack([pts, col.astype(np.float64)]))
+
+
+def test_filter_outliers_crafted_vs_reference(pkg):
+    """filter_out_outlier (MVS2.py:132-158) where it does remove patches: the
+    host core the stage's opt-in filter runs (mvs_filter_outliers) on the 60
+    crafted patch sets of tests/golden/filter_crafted.npz, recorded from the
+    reference's own CellTable (gen_golden.py --filter-crafted): the same
+    survivors, the same "remove a outlier" line count, ZeroDivisionError where
+    the reference raised it, and the survivors in reconstruct_from_Q's order
+    (MVS2.py:159-173: first sight in the (view, ci, cj) key walk = a stable
+    sort by (min view of V, cell))."""
+    g = dict(np.load(os.path.join(REPO, "tests", "golden", "filter_crafted.npz")))
+    cs, H, W = int(g["cs"]), int(g["H"]), int(g["W"])
+    nci, ncj = -(-(W - 1) // cs), -(-(H - 1) // cs)
+    n_rem = n_dz = 0
+    for k in range(int(g["n_cases"])):
+        mask, xy = g[f"c{k}_mask"], g[f"c{k}_xy"]
+        cell = np.floor(xy / cs).astype(np.int32)
+        count = np.array([bin(int(m)).count("1") for m in mask], np.int32)
+        args = (cell, mask.reshape(-1, 1), count, g[f"c{k}_avg"], g[f"c{k}_c"], g[f"c{k}_n"], nci, ncj)
+        if bool(g[f"c{k}_divzero"]):
+            with pytest.raises(ZeroDivisionError):
+                pkg._lib.filter_outliers(*args)
+            n_dz += 1
+            continue
+        alive, removed, lines = pkg._lib.filter_outliers(*args)
+        assert lines == int(g[f"c{k}_lines"]), k
+        assert removed == len(mask) - alive.sum()
+        minv = np.array([(int(m) & -int(m)).bit_length() - 1 for m in mask])
+        ids = np.nonzero(alive)[0]
+        order = sorted(ids, key=lambda e: (minv[e], cell[e, 0], cell[e, 1]))   # stable: fill order
+        assert order == g[f"c{k}_survivors"].tolist(), k
+        n_rem += removed > 0
+    assert n_rem >= 40 and n_dz >= 1
+
+
+def test_filter_outliers_bad_arguments(pkg):
+    with pytest.raises(RuntimeError):
+        pkg._lib.filter_outliers(np.zeros((1, 2)), np.ones(1, np.uint64), [1], [0.5], np.zeros(3), np.zeros(3), 0, 4)

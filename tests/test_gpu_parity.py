@@ -521,9 +521,9 @@ def test_bench_sweep_full_size(ctx, oracle_scene, dino, wid):
 
 
 def test_ring256_quarter_sweep(pkg, orc):
-    """SURVEY 8(d) config 4 scene (256 views, 1920x1080, uniform-random texture)
-    with a quarter of the bench sweep (2^18 candidates) on the view-group
-    scorer, against the oracle."""
+    """SURVEY 8(d) config 4 size (256 views, 1920x1080) on a uniform-random
+    texture with a quarter of the bench sweep (2^18 candidates) on the
+    view-group scorer, against the oracle (random textures: the reject path)."""
     import os
     syn = pkg.synthetic
     rgb, K, R, t = syn.ring_scene(256, 1080, 1920, seed=0)
@@ -535,6 +535,26 @@ def test_ring256_quarter_sweep(pkg, orc):
     for g, e in zip(got[:3], exp[:3]):
         assert np.array_equal(g, e)
     np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+
+
+def test_ring256_sphere_quarter_sweep(pkg, orc):
+    """The scene the bench's ring256 line times (synthetic.sphere_scene_device:
+    a textured sphere in 256 views of 1920x1080, where photo tests pass) with
+    2^18 candidates of the bench's distribution, against the oracle: masks,
+    counts and projections bit-exact, avg within 1e-12, and the pass path
+    really exercised (hundreds of thousands of passing (candidate, view) pairs)."""
+    import os
+    syn = pkg.synthetic
+    rgb, K, R, t = syn.sphere_scene_device(256, 1080, 1920, seed=0, device="cuda")
+    c, ref = syn.candidates(1 << 18, K, R, t, W=1920, H=1080, seed=0)
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        got = cx.score(c, ref, 0.7, 5)
+    sc = orc.Scene(rgb, K, R, t)
+    exp = sc.score_batch(c, ref, 0.7, 5, nthreads=min(os.cpu_count() or 1, 16))
+    for g, e in zip(got[:3], exp[:3]):
+        assert np.array_equal(g, e)
+    np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+    assert (got[2] >= 3).sum() > 10000 and got[2].sum() > 100000, (int((got[2] >= 3).sum()), int(got[2].sum()))
 
 
 @pytest.mark.parametrize("V,n", [(132, 2500), (160, 500), (160, 2500), (44, 600)])

@@ -6,7 +6,8 @@ against the oracle / the reference's golden vectors):
 * mvs_expand_candidates (MVS2.py:329-369) against the oracle, on the direct
   (< 2048 jobs) and the tiled (>= 2048) path;
 * 47 views at 640x480 (BASELINE config 3's view count, V % 16 != 0) at the
-  bench's candidate distribution and through a 2,000-pop stage;
+  bench's candidate distribution, through a 2,000-pop stage and through the
+  reference's full 100,000-pop expansion (oracle fixture);
 * images wider than 2048 pixels;
 * device calls on a caller's stream followed by host calls on the context's
   stream (the context's scratch is ordered across streams);
@@ -183,22 +184,39 @@ def test_view_count_47_bench_distribution(pkg, orc, dino47):
 def test_view_count_47_stage(pkg, orc, dino47, seeds):
     """The 47-view scene through a 2,000-pop stage (seeds restricted to
     tracks inside views 0-46), bit-exact against the oracle stage."""
+    from make_seeds import subset_seeds
     rgb, K, R, t = dino47
-    off, ov, oxy = seeds["track_off"], seeds["obs_view"], seeds["obs_xy"]
-    keep_off, keep_v, keep_xy = [0], [], []
-    for k in range(len(off) - 1):
-        v = ov[off[k]:off[k + 1]]
-        if (v < 47).all():
-            keep_v += list(v)
-            keep_xy += list(oxy[off[k]:off[k + 1]])
-            keep_off.append(len(keep_v))
-    args = (np.array(keep_off, np.int64), np.array(keep_v, np.int32), np.array(keep_xy, np.float32))
+    args = subset_seeds(seeds, 47)
     with pkg.MvsContext(rgb, K, R, t) as cx:
         ini, allp, st = cx.stage(*args, cell_size=2, scale=10.0, wid=5, max_pops=2000)
     oini, oall, ost = orc.Scene(rgb, K, R, t).mvs_stage(*args, scale=10.0, max_pops=2000)
     assert st["pops"] == ost["pops"] and st["tests"] == ost["tests"]
     assert np.array_equal(ini, oini) and np.array_equal(allp, oall)
     assert len(allp) > 1000
+
+
+def test_view_count_47_full_run_vs_oracle_fixture(pkg, dino47, seeds):
+    """BASELINE config 3 at full length: 47 views (templeRing is absent, so the
+    dinoRing subset of views 0-46 stands in) through the
+    reference's whole 100,000-pop expansion (MVS2.py:321).  Every accepted
+    patch, in order, against the oracle's full run
+    (tests/golden/gen_oracle_full.py 100000 47: counts + sha256 of both row
+    sets)."""
+    import hashlib
+    import json
+    import os
+    from conftest import GOLDEN
+    from make_seeds import subset_seeds
+    j = json.load(open(os.path.join(GOLDEN, "stage_oracle_v47_cap100000.json")))
+    rgb, K, R, t = dino47
+    with pkg.MvsContext(rgb, K, R, t) as cx:
+        ini, allp, st = cx.stage(*subset_seeds(seeds, 47), cell_size=2, scale=10.0, wid=5,
+                                 max_pops=100000)
+    for k in ("pops", "tests", "accepts", "queue_left"):
+        assert st[k] == j["stats"][k], k
+    assert len(ini) == j["n_initial"] and len(allp) == j["n_all"]
+    assert hashlib.sha256(np.ascontiguousarray(ini, "<f8").tobytes()).hexdigest() == j["sha256_initial"]
+    assert hashlib.sha256(np.ascontiguousarray(allp, "<f8").tobytes()).hexdigest() == j["sha256_all"]
 
 
 def test_wide_image(pkg, orc):
@@ -251,3 +269,51 @@ def test_timed_kernel_name(ctx, dino):
     ms, k = ctx.kernel_time()
     ctx.kernel_timing(False)
     assert k == 1 and ms > 0 and ctx.timed_kernel() == "k_score_mma"
+
+
+def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
+    """mvs_pack_accepted (the multi-GPU exchange's device pack, no host sync)
+    against parallel.pack_accepted_reference on the bench's 2^20 sweep:
+    identical header and rows, including a capacity below the accepted count
+    (the first cap rows, the true count in the header) and an empty slice.
+    The pack's device time is printed (budget: <= 10 us per 2^20 sweep)."""
+    import importlib
+    import torch
+    par = importlib.import_module(pkg.__name__ + ".parallel")
+    rgb, K, R, t = dino
+    n = 1 << 20
+    c, ref = bench_candidates(n, K, R, t, seed=0)
+    dev = torch.device("cuda:0")
+    tc, tr = torch.from_numpy(c).to(dev), torch.from_numpy(ref).to(dev)
+    xy = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    mask = torch.empty((n, 1), dtype=torch.int64, device=dev)
+    count = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.score_device(tc, tr, xy, mask, count, None, 0.7, 5)
+    torch.cuda.synchronize()
+    acc = int((count >= 3).sum())
+    assert acc > 1000
+    for cap, off in ((acc + 300, 5 << 20), (acc // 3, 0)):
+        out = torch.full((cap + 1, 5), -9, dtype=torch.int64, device=dev)
+        ctx.pack_accepted(off, count, mask, tc, 3, out)
+        exp = torch.full((cap + 1, 5), -9, dtype=torch.int64)
+        par.pack_accepted_reference(off, count.cpu(), mask.cpu(), tc.cpu(), 3, exp)
+        got = out.cpu()
+        k = min(acc, cap)
+        assert got[0, :3].tolist() == [acc, n, cap]
+        assert torch.equal(got[1:1 + k], exp[1:1 + k])
+    empty = torch.full((4, 5), -9, dtype=torch.int64, device=dev)
+    ctx.pack_accepted(0, count[:0], mask[:0], tc[:0], 3, empty)
+    assert empty[0, :3].cpu().tolist() == [0, 0, 3]
+    out = torch.empty((acc + 300 + 1, 5), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        ctx.pack_accepted(0, count, mask, tc, 3, out, stream=s.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(20):
+        ctx.pack_accepted(0, count, mask, tc, 3, out, stream=s.cuda_stream)
+    e1.record(s)
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / 20 * 1e3
+    print(f"pack_accepted: {us:.1f} us per 2^20 sweep ({acc} accepted rows)")
+    assert us < 100.0

@@ -1,9 +1,10 @@
 """The multi-rank sweep path (parallel.py) with world_size 2 and 3 on the gloo
 backend, CPU only.  The photo test inside each rank is the oracle here (the
-stand-in scorer for a CPU-only process; on the GPU box the same function runs
-with the HIP scorer over RCCL).  Checked: slices cover the batch exactly once,
-records round-trip, and every rank ends with the same accepted set as one
-process scoring the whole batch."""
+stand-in scorer for a CPU-only process; on the GPU box the HIP scorer and the
+device pack run over RCCL).  Checked: slices cover the batch exactly once,
+the stage driver delivers every rank's slice in order, and every rank ends
+each sweep with the same accepted set as one process scoring the whole
+batch."""
 import os
 import socket
 import sys
@@ -25,33 +26,6 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, out_dir):
-    import importlib
-    sys.path.insert(0, REPO)
-    sys.path.insert(0, GOLDEN)
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    par = importlib.import_module(PKG_NAME + ".parallel")
-    syn = importlib.import_module(PKG_NAME + ".synthetic")
-    from make_seeds import load_dino
-    from oracle import oracle as orc
-    imgs, K, R, t = load_dino(DATA)
-    sc = orc.Scene(np.stack(imgs), K, R, t)
-    c, ref = syn.candidates(n, K, R, t, seed=17)
-
-    def score_fn(cs, rs):
-        xy, mask, count, _ = sc.score_batch(cs.numpy(), rs.numpy(), 0.4, 5)
-        return torch.from_numpy(xy), torch.from_numpy(mask.view(np.int64)), torch.from_numpy(count)
-
-    idx, count, mask, xy = par.sharded_sweep(score_fn, torch.from_numpy(c), torch.from_numpy(ref),
-                                             vlb=3, words=1)
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), idx=idx.numpy(), count=count.numpy(),
-             mask=mask.numpy(), xy=xy.numpy())
-    dist.barrier()
-    dist.destroy_process_group()
-
-
 def test_shard_range_partitions():
     import importlib
     par = importlib.import_module(PKG_NAME + ".parallel")
@@ -63,25 +37,6 @@ def test_shard_range_partitions():
                 assert 0 <= b <= e <= n
                 cover += list(range(b, e))
             assert cover == list(range(n))
-
-
-@pytest.mark.parametrize("world,n", [(2, 600), (3, 401)])
-def test_sharded_sweep_gloo(tmp_path, orc, dino, world, n):
-    import importlib
-    syn = importlib.import_module(PKG_NAME + ".synthetic")
-    mp.spawn(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True)
-    rgb, K, R, t = dino
-    sc = orc.Scene(rgb, K, R, t)
-    c, ref = syn.candidates(n, K, R, t, seed=17)
-    xy, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
-    exp = np.nonzero(count >= 3)[0]
-    assert len(exp) > 0
-    for r in range(world):
-        z = np.load(tmp_path / f"r{r}.npz")
-        assert np.array_equal(z["idx"], exp)
-        assert np.array_equal(z["count"], count[exp])
-        assert np.array_equal(z["mask"].view(np.uint64), mask[exp])
-        assert np.array_equal(z["xy"], xy[exp])
 
 
 class _FakeStage:
@@ -162,59 +117,7 @@ def test_stage_sharded_driver_gloo(tmp_path, world):
         assert np.load(tmp_path / f"s{r}.npy").tolist() == [5, 8, 3, 1]
 
 
-def _compact_worker(rank, world, port, n, words, out_dir):
-    import importlib
-    sys.path.insert(0, REPO)
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    par = importlib.import_module(PKG_NAME + ".parallel")
-    rng = np.random.default_rng(100 + rank)          # this rank's own sweep slice (seed = rank)
-    mask = rng.integers(0, 2**63, (n, words), dtype=np.int64)
-    mask[rng.random((n, words)) < 0.5] = 0
-    mask[:, 0] |= np.int64(-2**63) * (rng.random(n) < 0.3)   # bit 63 set on some masks
-    cnt = np.array([sum(bin(int(w) & (2**64 - 1)).count("1") for w in row) for row in mask], np.int32)
-    blk = par.pack_compact(torch.from_numpy(cnt), torch.from_numpy(mask), 3)
-    blocks = par.all_gather_compact(blk)
-    idx, count, m = par.unpack_compact(blocks, n, words)
-    # the single-sync form the bench uses delivers the same blocks
-    blocks2 = par.exchange_accepted(torch.from_numpy(cnt), torch.from_numpy(mask), 3)
-    assert len(blocks2) == len(blocks)
-    for b1, b2 in zip(blocks, blocks2):
-        assert torch.equal(b1, b2)
-    np.savez(os.path.join(out_dir, f"c{rank}.npz"), idx=idx.numpy(), count=count.numpy(),
-             mask=m.numpy())
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,n,words", [(2, 1000, 1), (3, 130, 4)])
-def test_compact_exchange_gloo(tmp_path, world, n, words):
-    """The bench's per-sweep exchange (bitmap + masks of accepted candidates):
-    every rank rebuilds every rank's accepted (index, count, mask)."""
-    mp.spawn(_compact_worker, args=(world, _free_port(), n, words, str(tmp_path)), nprocs=world,
-             join=True)
-    exp_i, exp_c, exp_m = [], [], []
-    for r in range(world):
-        rng = np.random.default_rng(100 + r)
-        mask = rng.integers(0, 2**63, (n, words), dtype=np.int64)
-        mask[rng.random((n, words)) < 0.5] = 0
-        mask[:, 0] |= np.int64(-2**63) * (rng.random(n) < 0.3)
-        cnt = np.array([sum(bin(int(w) & (2**64 - 1)).count("1") for w in row) for row in mask])
-        acc = np.nonzero(cnt >= 3)[0]
-        exp_i.append(acc + r * n)
-        exp_c.append(cnt[acc])
-        exp_m.append(mask[acc])
-    exp_i, exp_c, exp_m = np.concatenate(exp_i), np.concatenate(exp_c), np.concatenate(exp_m)
-    assert len(exp_i) > 0
-    for r in range(world):
-        z = np.load(tmp_path / f"c{r}.npz")
-        assert np.array_equal(z["idx"], exp_i)
-        assert np.array_equal(z["count"], exp_c)
-        assert np.array_equal(z["mask"], exp_m)
-
-
-def _points_worker(rank, world, port, n, strong, out_dir):
+def _points_worker(rank, world, port, n, strong, sweeps, out_dir):
     import importlib
     sys.path.insert(0, REPO)
     sys.path.insert(0, GOLDEN)
@@ -227,47 +130,67 @@ def _points_worker(rank, world, port, n, strong, out_dir):
     from oracle import oracle as orc
     imgs, K, R, t = load_dino(DATA)
     sc = orc.Scene(np.stack(imgs), K, R, t)
-    if strong:      # one queue of n candidates, rank r scores its shard_range slice
-        c, ref = syn.candidates(n, K, R, t, seed=17)
-        b, e = par.shard_range(n, rank, world)
-        c, ref, off = c[b:e], ref[b:e], b
-    else:           # weak: block r of a queue of world * n candidates
-        c, ref = syn.candidates(n, K, R, t, seed=17 + rank)
-        off = rank * n
-    _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
-    rec = par.exchange_accepted_points(off, torch.from_numpy(count), torch.from_numpy(mask.view(np.int64)),
-                                       torch.from_numpy(np.ascontiguousarray(c)), 3)
-    idx, cnt, m, pts = par.unpack_points(rec, 1)
-    np.savez(os.path.join(out_dir, f"p{rank}.npz"), idx=idx.numpy(), count=cnt.numpy(), mask=m.numpy(),
-             pts=pts.numpy())
+    out = {}
+    ex = None
+    for k in range(sweeps):              # consecutive sweeps through the double buffers
+        seed = 17 + 100 * k
+        if strong:      # one queue of n candidates, rank r scores its shard_range slice
+            c, ref = syn.candidates(n, K, R, t, seed=seed)
+            b, e = par.shard_range(n, rank, world)
+            c, ref, off = c[b:e], ref[b:e], b
+        else:           # weak: block r of a queue of world * n candidates
+            c, ref = syn.candidates(n, K, R, t, seed=seed + rank)
+            off = rank * n
+        _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
+        if ex is None:
+            ex = par.PointsExchange(None, 1, n, torch.device("cpu"))
+        bi = ex.post(off, torch.from_numpy(count), torch.from_numpy(mask.view(np.int64)),
+                     torch.from_numpy(np.ascontiguousarray(c)), 3)
+        idx, m, pts = ex.result(bi)
+        out[f"idx{k}"], out[f"mask{k}"], out[f"pts{k}"] = idx.numpy(), m.numpy(), pts.numpy()
+    # capacity overflow is reported, not silently truncated
+    small = par.PointsExchange(None, 1, 2, torch.device("cpu"))
+    bi = small.post(0, torch.full((10,), 5, dtype=torch.int32), torch.ones((10, 1), dtype=torch.int64),
+                    torch.zeros((10, 3), dtype=torch.float64), 3)
+    try:
+        small.result(bi)
+        out["overflow_raised"] = np.array(False)
+    except RuntimeError:
+        out["overflow_raised"] = np.array(True)
+    np.savez(os.path.join(out_dir, f"p{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,n,strong", [(2, 500, False), (3, 401, True)])
 def test_accepted_points_exchange_gloo(tmp_path, orc, dino, world, n, strong):
-    """The bench's sweep exchange (bench.py, parallel.exchange_accepted_points):
-    the candidate queue split over the ranks -- per-rank blocks (weak) or
-    shard_range slices of one queue (strong) -- and every rank ends with the
-    whole sweep's accepted records, 3D points included, as one process
-    scoring the whole queue would produce them."""
+    """The bench's sweep exchange (bench.py, parallel.PointsExchange: device
+    pack layout, double-buffered all-gather): the candidate queue split over
+    the ranks -- per-rank blocks (weak) or shard_range slices of one queue
+    (strong) -- over three consecutive sweeps, and every rank ends each sweep
+    with the whole sweep's accepted candidates (|V| >= 3), masks and 3D points,
+    in index order, as one process scoring the whole queue finds them."""
     import importlib
     syn = importlib.import_module(PKG_NAME + ".synthetic")
-    mp.spawn(_points_worker, args=(world, _free_port(), n, strong, str(tmp_path)), nprocs=world, join=True)
+    sweeps = 3
+    mp.spawn(_points_worker, args=(world, _free_port(), n, strong, sweeps, str(tmp_path)), nprocs=world,
+             join=True)
     rgb, K, R, t = dino
     sc = orc.Scene(rgb, K, R, t)
-    if strong:
-        c, ref = syn.candidates(n, K, R, t, seed=17)
-    else:
-        parts = [syn.candidates(n, K, R, t, seed=17 + r) for r in range(world)]
-        c = np.concatenate([p[0] for p in parts])
-        ref = np.concatenate([p[1] for p in parts])
-    _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
-    exp = np.nonzero(count >= 3)[0]
-    assert len(exp) > 0
-    for r in range(world):
-        z = np.load(tmp_path / f"p{r}.npz")
-        assert np.array_equal(z["idx"], exp)
-        assert np.array_equal(z["count"], count[exp])
-        assert np.array_equal(z["mask"].view(np.uint64), mask[exp])
-        assert np.array_equal(z["pts"], c[exp])
+    for k in range(sweeps):
+        seed = 17 + 100 * k
+        if strong:
+            c, ref = syn.candidates(n, K, R, t, seed=seed)
+        else:
+            parts = [syn.candidates(n, K, R, t, seed=seed + r) for r in range(world)]
+            c = np.concatenate([p[0] for p in parts])
+            ref = np.concatenate([p[1] for p in parts])
+        _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
+        exp = np.nonzero(count >= 3)[0]
+        assert len(exp) > 0
+        for r in range(world):
+            z = np.load(tmp_path / f"p{r}.npz")
+            assert np.array_equal(z[f"idx{k}"], exp)
+            assert np.array_equal(z[f"mask{k}"].view(np.uint64), mask[exp])
+            assert np.array_equal(z[f"pts{k}"], c[exp])
+            assert bool(z["overflow_raised"])
