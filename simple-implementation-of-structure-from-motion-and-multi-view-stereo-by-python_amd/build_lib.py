@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmvs_amd.so")
 STAMPS_LIB = os.path.join(HERE, "libmvs_amd_stamps.so")   # diagnostic build (-DMVS_STAMPS)
+ASAN_LIB = os.path.join(HERE, "libmvs_amd_asan.so")       # host code under ASan + UBSan (tools/asan_cpu.sh)
 SOURCES = ["mvs_kernels.hip", "sfm_kernels.hip", "mvs_engine.cpp"]
 HEADERS = ["mvs_internal.h", "mvs_device.h", os.path.join("..", "..", "include", "mvs_amd.h")]
 ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
@@ -24,9 +25,9 @@ def needs_build():
     return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
 
 
-def build(force=False, verbose=False, stamps=False):
-    out = STAMPS_LIB if stamps else LIB
-    if not stamps and not force and not needs_build():
+def build(force=False, verbose=False, stamps=False, asan=False):
+    out = STAMPS_LIB if stamps else ASAN_LIB if asan else LIB
+    if not stamps and not asan and not force and not needs_build():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -36,6 +37,12 @@ def build(force=False, verbose=False, stamps=False):
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
     if stamps:
         cmd.append("-DMVS_STAMPS")
+    if asan:
+        # the host code only (the engine's commit, seeding, filter, sort
+        # bookkeeping, C-ABI checks); device code is never sanitized here
+        for f in ("-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                  "-fno-omit-frame-pointer", "-shared-libsan", "-g"):
+            cmd += ["-Xarch_host", f]
     # A/B of code-generation options (e.g. "-mllvm -amdgpu-sched-strategy=iterative-ilp")
     cmd += os.environ.get("MVS_EXTRA_FLAGS", "").split()
     cmd += ["-o", out + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
@@ -62,4 +69,5 @@ def check_undefined(path):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose=True, stamps="--stamps" in sys.argv,
+                asan="--asan" in sys.argv))

@@ -594,6 +594,7 @@ void filter_outliers_core(int64_t n, int words, int nci, int ncj, const int32_t*
 struct Engine {
     mvs_ctx* ctx;
     int V, words, cs, wid, vlb;
+    int flags = 0;   // mvs_stage_set_options at the stage's start
     double scale;
     int nci, ncj;
     int64_t max_pops;
@@ -1207,6 +1208,9 @@ Engine* make_engine(mvs_ctx* ctx, int cell_size, double scale, int wid, int64_t 
     E->ncj = (int)std::ceil((double)(ctx->H - 1) / cell_size);
     E->max_pops = std::min<int64_t>(std::max<int64_t>(max_pops, 0), 100000);   // MVS2.py:321
     E->s = ctx->stream;
+    // the stage's options are fixed when it starts (mvs_stage_set_options
+    // between mvs_stage_begin and mvs_stage_finish does not change it)
+    E->flags = ctx->stage_flags;
     // CellTable as vacancy bitmasks, one per cell: bit v of cell (ci, cj) = 1
     // while view v's cell is vacant (np.ones, MVS2.py:88)
     E->table.assign((size_t)E->nci * E->ncj * E->words, 0);
@@ -1225,7 +1229,7 @@ void finish_engine(mvs_ctx* ctx, Engine* E, mvs_stage_result* res) {
     HIPCHK(hipMemcpyAsync(&h, ctx->d_exact.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     const double t = Engine::now();
-    if (ctx->stage_flags & MVS_STAGE_FILTER_OUTLIERS) E->filter_outliers(res);
+    if (E->flags & MVS_STAGE_FILTER_OUTLIERS) E->filter_outliers(res);
     E->output(res);
     E->t_out[4] = Engine::now() - t;
     res->stats[7] = h;
@@ -1643,11 +1647,30 @@ int mvs_exact_avg(mvs_ctx* ctx, int64_t n, const int32_t* ref, const double* xy,
     if (n < 0 || (n > 0 && (!ref || !xy || !mask || !avg))) return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
     if (wid != 3 && wid != 5) return set_err(ctx, Fail{MVS_E_UNSUPPORTED, "exact avg supports wid 3 or 5"});
     return guarded(ctx, [&]() {
-        for (int64_t i = 0; i < n; ++i)
+        const int words = ctx->words();
+        for (int64_t i = 0; i < n; ++i) {
             if (ref[i] < 0 || ref[i] >= ctx->V) throw Fail{MVS_E_ARG, "ref view out of range"};
+            // a V list names other views (MVS2.py:66-67) inside the scene; a
+            // non-empty one needs a valid window (HarrisFeatures.py:128)
+            bool any = false;
+            for (int w = 0; w < words; ++w) {
+                uint64_t m = mask[i * words + w];
+                const int nv = ctx->V - 64 * w;
+                if (nv < 64 && (m >> nv)) throw Fail{MVS_E_ARG, "mask names a view >= V"};
+                if (ref[i] / 64 == w && ((m >> (ref[i] % 64)) & 1ull))
+                    throw Fail{MVS_E_ARG, "mask names the reference view itself"};
+                any |= m != 0;
+            }
+            if (any) {
+                const double x = xy[2 * i], y = xy[2 * i + 1];
+                if (!(x > -1e9 && x < 1e9 && y > -1e9 && y < 1e9)) throw Fail{MVS_E_ARG, "non-finite projection"};
+                const int q = (int)x, r = (int)y;
+                if (!(r - wid >= 0 && r + wid + 1 < ctx->H && q - wid > 0 && q + wid + 1 < ctx->W))
+                    throw Fail{MVS_E_ARG, "mask bits set for a window outside the image"};
+            }
+        }
         if (n == 0) return 0;
         hipStream_t s = ctx->stream;
-        const int words = ctx->words();
         ctx->s_ref.ensure(n); ctx->s_xy.ensure(n * 2); ctx->s_mask.ensure(n * words); ctx->s_avg.ensure(n);
         HIPCHK(hipMemcpyAsync(ctx->s_ref.p, ref, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(ctx->s_xy.p, xy, n * 2 * sizeof(double), hipMemcpyHostToDevice, s));

@@ -15,6 +15,7 @@
 // binary64 in the reference's order; this file is compiled with
 // -ffp-contract=off (products that numpy/OpenBLAS fuse are written as fma()).
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <utility>
 
@@ -1865,12 +1866,14 @@ __global__ __launch_bounds__(256) void k_exact_avg(const SceneDev sc, const Reco
     const int words = (sc.V + 63) >> 6;
     const int R = rec.R[r];
     int q = 0, rr = 0;
-    const bool ok = py_trunc(rec.xy[2 * r], &q) && py_trunc(rec.xy[2 * r + 1], &rr);
+    // a window outside the image has no passing views (its V list is empty);
+    // masked views of such a record read a defined NaN, never the stack
+    const bool ok = window_ok(sc, rec.xy[2 * r], rec.xy[2 * r + 1], WID, &q, &rr);
 #pragma unroll
     for (int sl = 0; sl < NS; ++sl) {
         const int v = lane + 64 * sl;
-        if (ok && v < sc.V && ((rec.mask[r * words + (v >> 6)] >> (v & 63)) & 1ull))
-            s_ncc[w][v] = exact_ncc_stack<WID>(sc, R, v, q, rr);
+        if (v < sc.V && ((rec.mask[r * words + (v >> 6)] >> (v & 63)) & 1ull))
+            s_ncc[w][v] = ok ? exact_ncc_stack<WID>(sc, R, v, q, rr) : __builtin_nan("");
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1913,28 +1916,30 @@ int launch_score_w(const SceneDev* sc, const ScoreArgs* a, hipStream_t s, hipEve
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// hipFuncAttributeMaxDynamicSharedMemorySize of a kernel, set once per device
+// (a per-device bit per kernel; racing first launches from two threads may
+// both set it, which is harmless)
+inline int set_dyn_lds_once(const void* f, std::atomic<uint64_t>& done, int lds) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    const uint64_t bit = dev < 64 ? (1ull << dev) : 0ull;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return 0;
+    if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
+    done.fetch_or(bit, std::memory_order_release);
+    return 0;
+}
+
 template <int WID, int NBLK, bool GROUPED>
 int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s) {
-    static bool attr = false;
+    static std::atomic<uint64_t> attr_fast{0}, attr_slow{0};
     if constexpr (GROUPED) {
         constexpr int lds = v_lds().total;
         if (fabs(a->thr) >= 0.01) {
-            if (!attr) {
-                if (hipFuncSetAttribute((const void*)k_score_mma_v<WID, true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-                    return -1;
-                attr = true;
-            }
+            if (set_dyn_lds_once((const void*)k_score_mma_v<WID, true>, attr_fast, lds) != 0) return -1;
             hipLaunchKernelGGL((k_score_mma_v<WID, true>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc, *a, *t,
                                (const int4*)t->items, (const int2*)t->sorted);
         } else {
-            static bool attr_slow = false;
-            if (!attr_slow) {
-                if (hipFuncSetAttribute((const void*)k_score_mma_v<WID, false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-                    return -1;
-                attr_slow = true;
-            }
+            if (set_dyn_lds_once((const void*)k_score_mma_v<WID, false>, attr_slow, lds) != 0) return -1;
             hipLaunchKernelGGL((k_score_mma_v<WID, false>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc, *a, *t,
                                (const int4*)t->items, (const int2*)t->sorted);
         }
@@ -1943,22 +1948,11 @@ int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipSt
         const int lds = mma_layout<WID, NBLK>(16 * NBLK).total;
         const int used = mma_layout<WID, NBLK>(sc->V).total;
         if (fabs(a->thr) >= 0.01) {
-            if (!attr) {
-                if (hipFuncSetAttribute((const void*)k_score_mma<WID, NBLK, true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-                    return -1;
-                attr = true;
-            }
+            if (set_dyn_lds_once((const void*)k_score_mma<WID, NBLK, true>, attr_fast, lds) != 0) return -1;
             hipLaunchKernelGGL((k_score_mma<WID, NBLK, true>), dim3(kMmaGrid), dim3(kMmaThreads), used, s, *sc, *a,
                                *t, (const int4*)t->items, (const int2*)t->sorted);
         } else {
-            static bool attr_slow = false;
-            if (!attr_slow) {
-                if (hipFuncSetAttribute((const void*)k_score_mma<WID, NBLK, false>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-                    return -1;
-                attr_slow = true;
-            }
+            if (set_dyn_lds_once((const void*)k_score_mma<WID, NBLK, false>, attr_slow, lds) != 0) return -1;
             hipLaunchKernelGGL((k_score_mma<WID, NBLK, false>), dim3(kMmaGrid), dim3(kMmaThreads), used, s, *sc,
                                *a, *t, (const int4*)t->items, (const int2*)t->sorted);
         }

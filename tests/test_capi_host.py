@@ -106,3 +106,16 @@ def test_filter_outliers_crafted_vs_reference(pkg):
 def test_filter_outliers_bad_arguments(pkg):
     with pytest.raises(RuntimeError):
         pkg._lib.filter_outliers(np.zeros((1, 2)), np.ones(1, np.uint64), [1], [0.5], np.zeros(3), np.zeros(3), 0, 4)
+
+
+def test_sanitizer_builds_when_requested(pkg, orc):
+    """Under tools/asan_cpu.sh (MVS_LIB / MVS_ORACLE_LIB name the ASan + UBSan
+    builds) the process really runs them: both libraries and the sanitizer
+    runtime are mapped."""
+    if "asan" not in os.environ.get("MVS_LIB", "") and "asan" not in os.environ.get("MVS_ORACLE_LIB", ""):
+        pytest.skip("not a sanitizer run")
+    pkg._lib.load()
+    orc.lib()
+    maps = open("/proc/self/maps").read()
+    assert "libmvs_amd_asan.so" in maps and "libmvs_oracle_asan.so" in maps
+    assert "libclang_rt.asan" in maps

@@ -212,7 +212,7 @@ def test_view_count_47_full_run_vs_oracle_fixture(pkg, dino47, seeds):
     with pkg.MvsContext(rgb, K, R, t) as cx:
         ini, allp, st = cx.stage(*subset_seeds(seeds, 47), cell_size=2, scale=10.0, wid=5,
                                  max_pops=100000)
-    for k in ("pops", "tests", "accepts", "queue_left"):
+    for k in ("pops", "tests", "queue_left"):
         assert st[k] == j["stats"][k], k
     assert len(ini) == j["n_initial"] and len(allp) == j["n_all"]
     assert hashlib.sha256(np.ascontiguousarray(ini, "<f8").tobytes()).hexdigest() == j["sha256_initial"]
