@@ -28,7 +28,9 @@ stay short):
   ring256      SURVEY 8(d) config 4: 256 views of 1920x1080 (a textured sphere,
                rendered on the GPU so that sweeps accept candidates), 2^20
                candidates per sweep, view-group scorer
-  cpu_baseline the oracle (C port of the reference arithmetic) on the host cores
+  cpu_baseline the oracle (C port of the reference arithmetic) on the host cores,
+               and beside it the reference's own single-core Python rate recorded
+               at fixture generation (tests/golden/reference_timing.json)
 
 python bench.py [--gpus N --steps K --warmup W --n CANDS --wid 5]
 N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -377,6 +379,18 @@ def main():
             "value_all_cores": m / cdt_all, "cores_all": ncores,
             "parity_on_sample": bool(np.array_equal(cnt_gpu, ocount) and
                                      np.array_equal(sw["mask"][:m].cpu().numpy().view(np.uint64), omask))}
+        # the reference itself (CPython, single thread): its recorded wall time
+        # for the longest unfiltered fixture run and the photo tests that run
+        # performed (tests/golden/gen_ref_timing.py)
+        rt = json.load(open(os.path.join(REPO, "tests", "golden", "reference_timing.json")))
+        run = max((r for r in rt["runs"] if "filter" not in r["fixture"]), key=lambda r: r["photo_tests"])
+        out["cpu_baseline"]["reference_python"] = {
+            "value": run["photo_tests_per_s"], "unit": "candidates/s", "cores": 1, "kind": "reference",
+            "sample": f"DensePointsWithMVS2 on dinoRing + seeds_dino.npz to {run['pops']} pops: "
+                      f"{run['photo_tests']} photo tests (MVS2.py:255 + :362) in {run['ref_seconds']:.0f} s",
+            "provenance": "build container (8-core Xeon), 1 core, measured at fixture generation "
+                          f"(tests/golden/gen_golden.py; {run['fixture']}); the reference does not travel "
+                          "to the GPU box"}
         if not out["cpu_baseline"]["parity_on_sample"]:
             print("WARNING: GPU/oracle mismatch on the cpu-baseline sample", file=sys.stderr)
     else:

@@ -581,8 +581,8 @@ __device__ unsigned long long g_stamps[4096 * 8];
 #endif
 
 struct alignas(16) CandInfo {
-    int32_t px, R, Sa, idx;   // table row of its pixel (px * views per row), reference view (-1: no
-                              // candidate), -S_a, batch index
+    int32_t osb, ow, Sa, R;   // LDS byte offsets of its pixel's S_b and w table rows, -S_a,
+                              // reference view (-1: no candidate)
     float T, gT;              // decision threshold on num w_b and its guard band
     double ca;                // n / (n-1) * w_a
 };
@@ -689,6 +689,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     __shared__ int s_ids[2];
     __shared__ int s_V;
     __shared__ double s_recip[65];
+    // the item's candidates are reordered by pixel row inside the tile (a
+    // counting sort in LDS): per (wave, row) counts and destination offsets
+    __shared__ uint8_t s_rcnt[kMmaWaves][MVS_TILE_H];
+    __shared__ int16_t s_roff[kMmaWaves][MVS_TILE_H];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int V = sc.V;
@@ -788,6 +792,21 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             const int Vl = s_V;
             const int h_rho0 = tid / Vl, h_v0 = tid - h_rho0 * Vl;
             const bool m2 = tid < Vl * 16;
+            // sort of the candidates by pixel row (rrel), stable: thread k holds
+            // candidate k; its rank among the wave's candidates of its row now,
+            // the destination after the offsets are known (phase 2 barriers)
+            int2 my_c = make_int2(0, 0);
+            int my_row = MVS_TILE_H, my_rank = 0;
+            if (tid < nc) {
+                my_c = ((const int2*)cand_buf(buf))[tid];
+                my_row = (my_c.y >> 4) & 7;
+            }
+            static_for<MVS_TILE_H>([&](auto Yc) {
+                constexpr int y = Yc;
+                const uint64_t bm = __ballot(my_row == y);
+                if (my_row == y) my_rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                if (lane == 0) s_rcnt[wave][y] = (uint8_t)__popcll(bm);
+            });
             // ---- 2. S_b and w of every view at the tile's pixels ----
             // horizontal sums of each region row on the unsigned bytes g = s + 128
             // (the moments are shift invariant): prefix sums by v_sad_u8 and
@@ -825,6 +844,25 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             }
             __syncthreads();
             STAMP(t1a);
+            // destination offsets of the row sort: row y's candidates start after
+            // every candidate of rows < y, then by wave
+            if (wave == kMmaWaves - 1 && lane < MVS_TILE_H) {
+                int tot = 0;
+#pragma unroll
+                for (int w = 0; w < kMmaWaves; ++w) tot += s_rcnt[w][lane];
+                int ex = tot;
+#pragma unroll
+                for (int off = 1; off < MVS_TILE_H; off <<= 1) {
+                    const int yv = __shfl_up(ex, off, 64);
+                    if (lane >= off) ex += yv;
+                }
+                int run = ex - tot;
+#pragma unroll
+                for (int w = 0; w < kMmaWaves; ++w) {
+                    s_roff[w][lane] = (int16_t)run;
+                    run += s_rcnt[w][lane];
+                }
+            }
             // vertical sums -> (S_b of s, w) per (pixel, view); the table overwrites
             // the horizontal sums, so every thread reads first
             int ms[MVS_TILE_H];
@@ -865,6 +903,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             }
             __syncthreads();
             STAMP(t1b);
+            if (tid < nc) ((int2*)cand_buf(buf))[s_roff[wave][my_row] + my_rank] = my_c;
             if (m2)
     #pragma unroll
                 for (int y = 0; y < MVS_TILE_H; ++y) {
@@ -908,6 +947,19 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 const bool valid = kk < nc;
                 const int2 e = valid ? cand[kk] : make_int2(-1, 0);
                 const int qrel = e.y & 15, rrel = (e.y >> 4) & 7, R = e.y >> 7;
+                // the block's candidates are sorted by row: its window rows span
+                // candidate 0's row to the last valid candidate's row + NB - 1, so
+                // only K-steps [s0, s0 + KSK) carry window rows when that span
+                // fits KSK = WID + 1 steps (always, for a block of one row)
+                const int last = min(15, nc - 1 - blk * 16);
+                const int r_lo = __builtin_amdgcn_readlane(rrel, 0);
+                const int r_hi = __builtin_amdgcn_readlane(rrel, last);
+                constexpr int KSK = WID + 1;
+                const int s_lo = r_lo >> 1, s_hi = (r_hi + NB - 1) >> 1;
+                // one pass of KSK steps when the span fits, else two (the second
+                // from s1, its steps already done read zero A rows)
+                const int npass = s_hi - s_lo < KSK ? 1 : 2;
+                const int s0 = min(s_lo, KS - KSK);
                 // A: the reference window, masked to candidate m's window columns
                 // (this lane's 16 columns) and rows (K-step rows in the window)
                 const uint32_t wm = valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u;
@@ -915,46 +967,53 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 uint32_t cm[4];
     #pragma unroll
                 for (int k4 = 0; k4 < 4; ++k4) cm[k4] = byte_mask((hm >> (4 * k4)) & 15u);
+                // bit 2s: K-step s holds a window row of this lane's row parity
                 const uint32_t rb = valid ? (((1u << NB) - 1u) << rrel) >> (kh >> 1) : 0u;
                 const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
-                const uint8_t* aptr = reg + R * VS + lofs;
-                const uint8_t* bptr[NBLK];
-    #pragma unroll
-                for (int nb = 0; nb < NBLK; ++nb) bptr[nb] = reg + min(16 * nb + m, V - 1) * VS + lofs;
                 v4i C[NBLK];
     #pragma unroll
                 for (int nb = 0; nb < NBLK; ++nb) C[nb] = (v4i){0, 0, 0, 0};
+                for (int pass = 0; pass < npass; ++pass) {
+                    const int sb = pass == 0 ? s0 : min(s0 + KSK, KS - KSK);
+                    const uint32_t rbp = (pass == 0 ? rb : rb & ~((1u << (2 * (s0 + KSK))) - 1u)) >> (2 * sb);
+                    const uint8_t* aptr = reg + R * VS + lofs + 64 * sb;
+                    const uint8_t* bptr[NBLK];
     #pragma unroll
-                for (int s = 0; s < KS; ++s) {
-                    const bool rv = (rb >> (2 * s)) & 1u;
-                    // rows outside the window read 16 zero bytes: an address select
-                    // instead of a branch around the load
-                    const uint4 av = *(const uint4*)(rv ? aptr + 64 * s : zrow);
-                    const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]),
-                                   (int)(av.w & cm[3])};
+                    for (int nb = 0; nb < NBLK; ++nb) bptr[nb] = reg + min(16 * nb + m, V - 1) * VS + lofs + 64 * sb;
     #pragma unroll
-                    for (int nb = 0; nb < NBLK; ++nb) {
-                        const uint4 bv = *(const uint4*)(bptr[nb] + 64 * s);
-                        const v4i B = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
-                        C[nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, C[nb], 0, 0, 0);
+                    for (int s = 0; s < KSK; ++s) {
+                        const bool rv = (rbp >> (2 * s)) & 1u;
+                        // rows outside the window read 16 zero bytes: an address select
+                        // instead of a branch around the load
+                        const uint4 av = *(const uint4*)(rv ? aptr + 64 * s : zrow);
+                        const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]),
+                                       (int)(av.w & cm[3])};
+    #pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) {
+                            const uint4 bv = *(const uint4*)(bptr[nb] + 64 * s);
+                            const v4i B = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
+                            C[nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, C[nb], 0, 0, 0);
+                        }
                     }
                 }
                 // candidate m's constants (row 0 of the wave), shared through LDS
-                double my_ca = 0.0;
+                double my_ca = 0.0, my_wa = 0.0;
                 if (kh == 0) {
                     CandInfo c;
-                    c.px = (e.y & 127) * VP;             // (rrel * 16 + qrel) * VP
-                    const int o = c.px + R;
+                    const int px = e.y & 127;            // rrel * 16 + qrel
+                    const int o = px * VP + R;
                     const double wa = tw[o];
-                    c.R = valid ? R : -1;
+                    c.osb = L.sb + px * VP * 4;          // byte offsets of the pixel's table rows:
+                    c.ow = L.w + px * VP * 8;            // S_b (int32) and w (binary64)
                     c.Sa = -tsb[o];                      // -S_a: num = n C + (-S_a) S_b
-                    c.idx = e.x;
+                    c.R = valid ? R : -1;
                     // T = thr (n-1)/n sqrt(da) in binary32 (1-ulp reciprocal, well inside the guard band)
                     c.T = valid ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf("");
                     c.gT = 2e-6f * fabsf(c.T);
                     c.ca = kn * wa;
                     ci[m] = c;
                     my_ca = c.ca;
+                    my_wa = wa;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -964,37 +1023,38 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 static_for<4>([&](auto Ic) {
                     constexpr int i = Ic;
                     const CandInfo c = ci[4 * kh + i];
+                    const int32_t* sbp = (const int32_t*)(smem + c.osb) + m;
+                    const double* twp = (const double*)(smem + c.ow) + m;
                     double sa = 0.0;
                     uint64_t g = 0;
                     static_for<NBLK>([&](auto Nc) {
                         constexpr int nb = Nc;
                         const int vl = 16 * nb + m;
-                        const int o = c.px + vl;
-                        const int num = __mul24(c.Sa, tsb[o]) + __mul24(NPX, C[nb][i]);
-                        const double w = tw[o];
-                        // lane masks straight from v_cmp (a ballot of a bool would
-                        // round-trip it through a VGPR)
-                        const uint64_t liv = __builtin_amdgcn_uicmp((uint32_t)vl, (uint32_t)c.R, 33);   // ne
-                        bool pass;
+                        const int num = __mul24(c.Sa, sbp[16 * nb]) + __mul24(NPX, C[nb][i]);
+                        const double w = twp[16 * nb];
                         uint64_t P;
                         if constexpr (FAST) {
-                            // ncc > thr <=> num w_b > T; w_b nan (constant window) never passes
-                            const float wf = WF ? twf[o] : (float)w;
-                            const float x = fmaf((float)num, wf, -c.T);
-                            P = __builtin_amdgcn_fcmpf(x, 0.0f, 2) & liv;                   // ogt
-                            // the lane's bit of P as the select condition of the sum
-                            // (the compares are not evaluated a second time)
-                            pass = __builtin_amdgcn_inverse_ballot_w64(P);
-                            g |= __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4) & liv;           // olt
+                            // ncc > thr <=> num w_b > T; w_b nan (constant window) never
+                            // passes.  The candidate's own view R passes too (its ncc is
+                            // n/(n-1) > thr): its mask bit and its term of the sum are
+                            // taken out once per candidate (no per-pair view test)
+                            const float x = fmaf((float)num, (float)w, -c.T);
+                            P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
+                            // the lane's bit of P as the select of the sum (the compare
+                            // is not evaluated a second time); the int select before
+                            // the conversion
+                            const int nm = __builtin_amdgcn_inverse_ballot_w64(P) ? num : 0;
+                            g |= __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4);                  // olt
+                            sa = fma((double)nm, w, sa);
                         } else {
                             const double ncc = (double)num * w * c.ca;
-                            pass = vl != c.R && ncc > a.thr;
+                            const bool pass = vl != c.R && ncc > a.thr;
                             P = __ballot(pass);
                             g |= __ballot(vl != c.R && fabs(ncc - a.thr) <= kGuard);
+                            sa = fma((double)num, pass ? w : 0.0, sa);
                         }
                         pmv = writelane<2 * (i * NBLK + nb)>(pmv, (uint32_t)P);
                         pmv = writelane<2 * (i * NBLK + nb) + 1>(pmv, (uint32_t)(P >> 32));
-                        sa = fma((double)num, pass ? w : 0.0, sa);
                     });
                     gdv = writelane<2 * i>(gdv, (uint32_t)g);
                     gdv = writelane<2 * i + 1>(gdv, (uint32_t)(g >> 32));
@@ -1015,12 +1075,22 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                     uint64_t mk = 0;
     #pragma unroll
                     for (int nb = 0; nb < NBLK; ++nb) mk |= (uint64_t)pm16[4 * (i * NBLK + nb) + j] << (16 * nb);
+                    // the reference view itself is no V entry (MVS2.py:66-67)
+                    const uint64_t self = (mk >> R) & 1ull;
+                    mk &= ~(1ull << R);
                     const uint32_t gg = ((const uint16_t*)wp->gd)[4 * i + j];
                     const int cnt = __popcll(mk);
                     const int64_t idx = e.x;
                     a.mask[idx] = mk;
                     a.count[idx] = cnt;
-                    if (a.avg) a.avg[idx] = cnt ? wp->wsum[m] * my_ca * s_recip[cnt] : 0.0;
+                    if (a.avg) {
+                        // its own term num_RR w_a = D_a w_a = sqrt(D_a) = 1 / w_a (to the
+                        // rsq + Newton accuracy of w_a, 4e-15) leaves the sum
+                        double inv = __builtin_amdgcn_rcp(my_wa);
+                        inv = inv * (2.0 - my_wa * inv);
+                        const double sum = self ? wp->wsum[m] - inv : wp->wsum[m];
+                        a.avg[idx] = cnt ? sum * my_ca * s_recip[cnt] : 0.0;
+                    }
                     if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
                 }
             }
