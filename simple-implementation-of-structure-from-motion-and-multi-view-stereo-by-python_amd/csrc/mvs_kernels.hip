@@ -529,6 +529,13 @@ struct MmaGeom {
     static_assert(ROWS % 2 == 0, "K-steps take two rows");
 };
 
+// x through an opaque copy: what is computed from it is computed where it is
+// used, not hoisted out of loops into long-lived registers
+DEV int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // 4-bit column mask -> byte mask
 DEV uint32_t byte_mask(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xffu; }
 
@@ -580,24 +587,18 @@ __device__ unsigned long long g_stamps[4096 * 8];
 #define STAMP_ADD_W0(slot, val)
 #endif
 
+// a candidate's constants in phase 3 (per wave, 32 slots: the two M-blocks
+// of its unit)
 struct alignas(16) CandInfo {
-    int32_t osb, ow, Sa, R;   // LDS byte offsets of its pixel's S_b and w table rows, -S_a,
-                              // reference view (-1: no candidate)
-    float T, gT;              // decision threshold on num w_b and its guard band
-    double ca;                // n / (n-1) * w_a
-};
-
-// per-wave slot: ballots (pass per (i, nb), guard per i) and the candidates' sums
-template <int NBLK>
-struct WaveSlot {
-    uint32_t pm[2 * 4 * NBLK];
-    uint32_t gd[8];
-    double wsum[16];
+    int32_t osb;              // LDS byte offset of its pixel's S_b table row (the w row follows from it)
+    int32_t Sa;               // -S_a
+    int32_t R;                // reference view (-1: no candidate)
+    float T;                  // decision threshold on num w_b (FAST: binary32; else thr)
 };
 
 // LDS layout: region | S_b table, w table (binary64), [w table (binary32)]
 // (the tables alias the horizontal sums of phase 2) | per-wave candidate
-// slots | per-wave ballots and sums | the item's candidates | 32 zero bytes
+// slots | the item's candidates | 32 zero bytes
 struct MmaLds {
     int reg, regsz, sb, w, wf, ci, wp, cand, zero, total;
 };
@@ -619,8 +620,8 @@ __host__ __device__ constexpr MmaLds mma_lds(int V) {
     L.wf = L.w + 128 * VP * 8;
     const int htmp = G::ROWS * 16 * VP * 4, tab = 128 * VP * (WF ? 16 : 12);
     L.ci = L.sb + (htmp > tab ? htmp : tab);
-    L.wp = L.ci + kMmaWaves * 16 * (int)sizeof(CandInfo);
-    L.cand = L.wp + kMmaWaves * (int)sizeof(WaveSlot<NBLK>);
+    L.wp = L.ci + kMmaWaves * 32 * (int)sizeof(CandInfo);
+    L.cand = L.wp;
     L.zero = L.cand + (DB ? 0 : kMmaChunk * 8);
     L.total = L.zero + 32;
     return L;
@@ -629,7 +630,8 @@ __host__ __device__ constexpr MmaLds mma_lds(int V) {
 // static LDS of k_score_mma: region and candidate buffers (DB) + small slots
 template <int WID, int NBLK, bool DB>
 __host__ __device__ constexpr int mma_static_lds() {
-    return (DB ? 2 * (16 * NBLK * MmaGeom<WID>::VS + kMmaChunk * 8) : 64) + 8 + 4 + 65 * 8 + 64;
+    return (DB ? 2 * (16 * NBLK * MmaGeom<WID>::VS + kMmaChunk * 8) : 64) + 8 + 4 + 65 * 8 + 64 +
+           MVS_TILE_H * kMmaWaves * 3;   // the row sort's counts and offsets
 }
 
 // what fits in 160 KiB beside the rest at this NBLK (1 workgroup of 16 waves
@@ -691,8 +693,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     __shared__ double s_recip[65];
     // the item's candidates are reordered by pixel row inside the tile (a
     // counting sort in LDS): per (wave, row) counts and destination offsets
-    __shared__ uint8_t s_rcnt[kMmaWaves][MVS_TILE_H];
-    __shared__ int16_t s_roff[kMmaWaves][MVS_TILE_H];
+    __shared__ __attribute__((aligned(16))) uint8_t s_rcnt[MVS_TILE_H][kMmaWaves];
+    __shared__ __attribute__((aligned(16))) int16_t s_roff[MVS_TILE_H][kMmaWaves];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int V = sc.V;
@@ -704,8 +706,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     int32_t* tsb = (int32_t*)(smem + L.sb);
     double* tw = (double*)(smem + L.w);
     float* twf = (float*)(smem + L.wf);
-    CandInfo* ci = (CandInfo*)(smem + L.ci) + wave * 16;
-    WaveSlot<NBLK>* wp = (WaveSlot<NBLK>*)(smem + L.wp) + wave;
+    CandInfo* ci = (CandInfo*)(smem + L.ci) + wave * 32;
     if (tid < 8) ((uint32_t*)(smem + L.zero))[tid] = 0u;
     const uint8_t* zrow = smem + L.zero;
 
@@ -801,12 +802,14 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 my_c = ((const int2*)cand_buf(buf))[tid];
                 my_row = (my_c.y >> 4) & 7;
             }
+            int my_cnt = 0;   // lane y < 8: the wave's count of row y
             static_for<MVS_TILE_H>([&](auto Yc) {
                 constexpr int y = Yc;
                 const uint64_t bm = __ballot(my_row == y);
                 if (my_row == y) my_rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-                if (lane == 0) s_rcnt[wave][y] = (uint8_t)__popcll(bm);
+                my_cnt = writelane<y>((uint32_t)my_cnt, (uint32_t)__popcll(bm));
             });
+            if (lane < MVS_TILE_H) s_rcnt[lane][wave] = (uint8_t)my_cnt;
             // ---- 2. S_b and w of every view at the tile's pixels ----
             // horizontal sums of each region row on the unsigned bytes g = s + 128
             // (the moments are shift invariant): prefix sums by v_sad_u8 and
@@ -845,23 +848,31 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             __syncthreads();
             STAMP(t1a);
             // destination offsets of the row sort: row y's candidates start after
-            // every candidate of rows < y, then by wave
+            // every candidate of rows < y, then by wave (lane y of the last wave:
+            // the row's 16 wave counts in one read, prefix sums in registers)
             if (wave == kMmaWaves - 1 && lane < MVS_TILE_H) {
+                const uint4 q4 = *(const uint4*)&s_rcnt[lane][0];
+                const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+                int pre[kMmaWaves];
                 int tot = 0;
-#pragma unroll
-                for (int w = 0; w < kMmaWaves; ++w) tot += s_rcnt[w][lane];
+    #pragma unroll
+                for (int w = 0; w < kMmaWaves; ++w) {
+                    pre[w] = tot;
+                    tot += (qw[w >> 2] >> (8 * (w & 3))) & 0xff;
+                }
                 int ex = tot;
-#pragma unroll
+    #pragma unroll
                 for (int off = 1; off < MVS_TILE_H; off <<= 1) {
                     const int yv = __shfl_up(ex, off, 64);
                     if (lane >= off) ex += yv;
                 }
-                int run = ex - tot;
-#pragma unroll
-                for (int w = 0; w < kMmaWaves; ++w) {
-                    s_roff[w][lane] = (int16_t)run;
-                    run += s_rcnt[w][lane];
-                }
+                const int base = ex - tot;
+                uint32_t pk[kMmaWaves / 2];
+    #pragma unroll
+                for (int w = 0; w < kMmaWaves / 2; ++w)
+                    pk[w] = (uint32_t)(base + pre[2 * w]) | ((uint32_t)(base + pre[2 * w + 1]) << 16);
+                *(uint4*)&s_roff[lane][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                *(uint4*)&s_roff[lane][8] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
             }
             // vertical sums -> (S_b of s, w) per (pixel, view); the table overwrites
             // the horizontal sums, so every thread reads first
@@ -889,7 +900,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         q += Q[y + NB - 1] - Q[y - 1];
                     }
                     const int db = NPX * q - sg * sg;   // < 2^31: n * sum g^2 <= 121 * 121 * 255^2
-                    double w = __builtin_nan("");       // constant window: ctNcc's nan
+                    // constant window: ctNcc's nan, never passes.  FAST stores 0
+                    // instead (num w_b = 0 < T there too), so that a rejected
+                    // pair's zero term of the avg sum stays zero
+                    double w = FAST ? 0.0 : __builtin_nan("");
                     if (db > 0) {
                         // v_rsq_f64 + one Newton step: max relative error 4.1e-15 over
                         // 4M values of D < 2^31 (tools/ubench/rsq_acc.hip; 5.2e-8 without)
@@ -903,7 +917,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             }
             __syncthreads();
             STAMP(t1b);
-            if (tid < nc) ((int2*)cand_buf(buf))[s_roff[wave][my_row] + my_rank] = my_c;
+            if (tid < nc) ((int2*)cand_buf(buf))[s_roff[my_row][wave] + my_rank] = my_c;
             if (m2)
     #pragma unroll
                 for (int y = 0; y < MVS_TILE_H; ++y) {
@@ -916,8 +930,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 for (int k = tid; k < 128 * (VP - V); k += kMmaThreads) {
                     const int px = k / (VP - V), v = V + (k - px * (VP - V));
                     tsb[px * VP + v] = 0;
-                    tw[px * VP + v] = __builtin_nan("");
-                    if constexpr (WF) twf[px * VP + v] = __builtin_nanf("");
+                    tw[px * VP + v] = FAST ? 0.0 : __builtin_nan("");
+                    if constexpr (WF) twf[px * VP + v] = FAST ? 0.0f : __builtin_nanf("");
                 }
             __syncthreads();
             STAMP(t2);
@@ -934,164 +948,238 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 if (tid == 0) pend = atomicAdd(head, 1);
             }
     
-            // ---- 3. + 4. the candidates, 16 per wave and M-block ----
+            // ---- 3. + 4. the candidates: a wave takes units of two M-blocks of
+            // 16 (32 consecutive candidates of the row-sorted list), which share
+            // their K-steps and B operands and give the epilogue two
+            // independent chains ----
             const int nblk = (nc + 15) >> 4;
+            const int nunit = (nblk + 1) >> 1;
     #ifdef MVS_STAMPS
             unsigned long long w0blk = 0;
     #endif
-            for (int blk = wave; blk < nblk; blk += kMmaWaves) {
+            for (int u = wave; u < nunit; u += kMmaWaves) {
     #ifdef MVS_STAMPS
-                ++w0blk;
+                w0blk += 2;
     #endif
-                const int kk = blk * 16 + m;
-                const bool valid = kk < nc;
-                const int2 e = valid ? cand[kk] : make_int2(-1, 0);
-                const int qrel = e.y & 15, rrel = (e.y >> 4) & 7, R = e.y >> 7;
-                // the block's candidates are sorted by row: its window rows span
-                // candidate 0's row to the last valid candidate's row + NB - 1, so
-                // only K-steps [s0, s0 + KSK) carry window rows when that span
-                // fits KSK = WID + 1 steps (always, for a block of one row)
-                const int last = min(15, nc - 1 - blk * 16);
-                const int r_lo = __builtin_amdgcn_readlane(rrel, 0);
-                const int r_hi = __builtin_amdgcn_readlane(rrel, last);
-                constexpr int KSK = WID + 1;
+                // lane constants recomputed per unit (hoisted, they would hold
+                // registers through phase 2)
+                const int ol = opaque(lane);
+                const int m = ol & 15, kh = ol >> 4;
+                int2 e[2];
+                bool valid[2];
+                int qrel[2], rrel[2], Rv[2];
+    #pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int kk = u * 32 + 16 * h + m;
+                    valid[h] = kk < nc;
+                    e[h] = valid[h] ? cand[kk] : make_int2(-1, 0);
+                    qrel[h] = e[h].y & 15;
+                    rrel[h] = (e[h].y >> 4) & 7;
+                    Rv[h] = e[h].y >> 7;
+                }
+                // the unit's candidates are sorted by row: its window rows span
+                // candidate 0's row to the last valid candidate's row + NB - 1
+                const int last = min(31, nc - 1 - u * 32);
+                const int r_lo = __builtin_amdgcn_readlane(rrel[0], 0);
+                const int r_hi = last >= 16 ? __builtin_amdgcn_readlane(rrel[1], last - 16)
+                                            : __builtin_amdgcn_readlane(rrel[0], last);
+                constexpr int KSK = WID + 1;     // K-steps of one row's windows
                 const int s_lo = r_lo >> 1, s_hi = (r_hi + NB - 1) >> 1;
-                // one pass of KSK steps when the span fits, else two (the second
-                // from s1, its steps already done read zero A rows)
-                const int npass = s_hi - s_lo < KSK ? 1 : 2;
-                const int s0 = min(s_lo, KS - KSK);
-                // A: the reference window, masked to candidate m's window columns
-                // (this lane's 16 columns) and rows (K-step rows in the window)
-                const uint32_t wm = valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u;
-                const uint32_t hm = wm >> (16 * (kh & 1));
-                uint32_t cm[4];
+                const int span = s_hi - s_lo + 1;
+                // A: the reference windows, masked to each candidate's window
+                // columns (this lane's 16 columns) and rows (bit 2s: K-step s holds
+                // a window row of this lane's row parity)
+                uint32_t cm[2][4], rb[2];
     #pragma unroll
-                for (int k4 = 0; k4 < 4; ++k4) cm[k4] = byte_mask((hm >> (4 * k4)) & 15u);
-                // bit 2s: K-step s holds a window row of this lane's row parity
-                const uint32_t rb = valid ? (((1u << NB) - 1u) << rrel) >> (kh >> 1) : 0u;
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t wm = valid[h] ? (((1u << NB) - 1u) << (qrel[h] + C0)) : 0u;
+                    const uint32_t hm = wm >> (16 * (kh & 1));
+    #pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) cm[h][k4] = byte_mask((hm >> (4 * k4)) & 15u);
+                    rb[h] = valid[h] ? (((1u << NB) - 1u) << rrel[h]) >> (kh >> 1) : 0u;
+                }
                 const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
-                v4i C[NBLK];
+                v4i C[2][NBLK];
     #pragma unroll
-                for (int nb = 0; nb < NBLK; ++nb) C[nb] = (v4i){0, 0, 0, 0};
-                for (int pass = 0; pass < npass; ++pass) {
-                    const int sb = pass == 0 ? s0 : min(s0 + KSK, KS - KSK);
-                    const uint32_t rbp = (pass == 0 ? rb : rb & ~((1u << (2 * (s0 + KSK))) - 1u)) >> (2 * sb);
-                    const uint8_t* aptr = reg + R * VS + lofs + 64 * sb;
+                for (int h = 0; h < 2; ++h)
+    #pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) C[h][nb] = (v4i){0, 0, 0, 0};
+                // NST K-steps from sb; steps below sd are done (their A rows read zeros)
+                auto kpass = [&](auto nstc, int sb, int sd) {
+                    constexpr int NST = decltype(nstc)::value;
+                    uint32_t rbp[2];
+                    const uint8_t* aptr[2];
+    #pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        rbp[h] = (rb[h] & ~((1u << (2 * sd)) - 1u)) >> (2 * sb);
+                        aptr[h] = reg + Rv[h] * VS + lofs + 64 * sb;
+                    }
                     const uint8_t* bptr[NBLK];
     #pragma unroll
                     for (int nb = 0; nb < NBLK; ++nb) bptr[nb] = reg + min(16 * nb + m, V - 1) * VS + lofs + 64 * sb;
+                    // operands of step st + 1 load while step st's MFMAs run; the
+                    // schedule barrier keeps the compiler from hoisting more loads
+                    // (their registers would spill)
+                    uint4 av[2][2], bv[2][NBLK];
+                    auto load = [&](int st, int slot) {
     #pragma unroll
-                    for (int s = 0; s < KSK; ++s) {
-                        const bool rv = (rbp >> (2 * s)) & 1u;
-                        // rows outside the window read 16 zero bytes: an address select
-                        // instead of a branch around the load
-                        const uint4 av = *(const uint4*)(rv ? aptr + 64 * s : zrow);
-                        const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]),
-                                       (int)(av.w & cm[3])};
+                        for (int h = 0; h < 2; ++h)
+                            // rows outside the window read 16 zero bytes: an address
+                            // select instead of a branch around the load
+                            av[slot][h] = *(const uint4*)(((rbp[h] >> (2 * st)) & 1u) ? aptr[h] + 64 * st : zrow);
+    #pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) bv[slot][nb] = *(const uint4*)(bptr[nb] + 64 * st);
+                    };
+                    load(0, 0);
+    #pragma unroll
+                    for (int st = 0; st < NST; ++st) {
+                        const int cur = st & 1;
+                        if (st + 1 < NST) load(st + 1, cur ^ 1);
+                        v4i A[2];
+    #pragma unroll
+                        for (int h = 0; h < 2; ++h)
+                            A[h] = (v4i){(int)(av[cur][h].x & cm[h][0]), (int)(av[cur][h].y & cm[h][1]),
+                                         (int)(av[cur][h].z & cm[h][2]), (int)(av[cur][h].w & cm[h][3])};
     #pragma unroll
                         for (int nb = 0; nb < NBLK; ++nb) {
-                            const uint4 bv = *(const uint4*)(bptr[nb] + 64 * s);
-                            const v4i B = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
-                            C[nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, C[nb], 0, 0, 0);
+                            const v4i B = {(int)bv[cur][nb].x, (int)bv[cur][nb].y, (int)bv[cur][nb].z, (int)bv[cur][nb].w};
+                            C[0][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B, C[0][nb], 0, 0, 0);
+                            C[1][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B, C[1][nb], 0, 0, 0);
                         }
+                        __builtin_amdgcn_sched_barrier(0);
                     }
+                };
+                if (span <= KSK) {
+                    kpass(std::integral_constant<int, KSK>{}, min(s_lo, KS - KSK), 0);
+                } else if (span == KSK + 1) {
+                    kpass(std::integral_constant<int, KSK + 1>{}, min(s_lo, KS - KSK - 1), 0);
+                } else {
+                    for (int sd = s_lo; sd <= s_hi; sd += KSK) kpass(std::integral_constant<int, KSK>{}, min(sd, KS - KSK), sd);
                 }
-                // candidate m's constants (row 0 of the wave), shared through LDS
-                double my_ca = 0.0, my_wa = 0.0;
+                // the candidates' constants (row 0 of the wave computes them for
+                // both blocks), shared through LDS
+                double my_ca[2] = {0.0, 0.0}, my_wa[2] = {0.0, 0.0};
                 if (kh == 0) {
-                    CandInfo c;
-                    const int px = e.y & 127;            // rrel * 16 + qrel
-                    const int o = px * VP + R;
-                    const double wa = tw[o];
-                    c.osb = L.sb + px * VP * 4;          // byte offsets of the pixel's table rows:
-                    c.ow = L.w + px * VP * 8;            // S_b (int32) and w (binary64)
-                    c.Sa = -tsb[o];                      // -S_a: num = n C + (-S_a) S_b
-                    c.R = valid ? R : -1;
-                    // T = thr (n-1)/n sqrt(da) in binary32 (1-ulp reciprocal, well inside the guard band)
-                    c.T = valid ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf("");
-                    c.gT = 2e-6f * fabsf(c.T);
-                    c.ca = kn * wa;
-                    ci[m] = c;
-                    my_ca = c.ca;
-                    my_wa = wa;
+    #pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        CandInfo c;
+                        const int px = e[h].y & 127;          // rrel * 16 + qrel
+                        const int o = px * VP + Rv[h];
+                        const double wa = tw[o];
+                        c.osb = L.sb + px * VP * 4;
+                        c.Sa = -tsb[o];                       // -S_a: num = n C + (-S_a) S_b
+                        c.R = valid[h] ? Rv[h] : -1;
+                        // FAST: T = thr (n-1)/n sqrt(da) in binary32 (1-ulp reciprocal,
+                        // well inside the guard band); else the decision is on ncc
+                        c.T = FAST ? (valid[h] ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf("")) : 0.0f;
+                        ci[16 * h + m] = c;
+                        my_ca[h] = kn * wa;
+                        my_wa[h] = wa;
+                    }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
-                // lane (kh, m) holds C[4 kh + i][16 nb + m]: candidate 4 kh + i, view 16 nb + m
-                uint32_t pmv = 0, gdv = 0;
-                double sacc[4];
+                // lane (kh, m) holds C[h][nb][i] = block h's candidate 4 kh + i, view 16 nb + m
+                uint32_t pmv[2] = {0u, 0u}, gdv[2] = {0u, 0u};
+                double sacc[2][4];
                 static_for<4>([&](auto Ic) {
                     constexpr int i = Ic;
-                    const CandInfo c = ci[4 * kh + i];
-                    const int32_t* sbp = (const int32_t*)(smem + c.osb) + m;
-                    const double* twp = (const double*)(smem + c.ow) + m;
-                    double sa = 0.0;
-                    uint64_t g = 0;
-                    static_for<NBLK>([&](auto Nc) {
-                        constexpr int nb = Nc;
-                        const int vl = 16 * nb + m;
-                        const int num = __mul24(c.Sa, sbp[16 * nb]) + __mul24(NPX, C[nb][i]);
-                        const double w = twp[16 * nb];
-                        uint64_t P;
-                        if constexpr (FAST) {
-                            // ncc > thr <=> num w_b > T; w_b nan (constant window) never
-                            // passes.  The candidate's own view R passes too (its ncc is
-                            // n/(n-1) > thr): its mask bit and its term of the sum are
-                            // taken out once per candidate (no per-pair view test)
-                            const float x = fmaf((float)num, (float)w, -c.T);
-                            P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
-                            // the lane's bit of P as the select of the sum (the compare
-                            // is not evaluated a second time); the int select before
-                            // the conversion
-                            const int nm = __builtin_amdgcn_inverse_ballot_w64(P) ? num : 0;
-                            g |= __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4);                  // olt
-                            sa = fma((double)nm, w, sa);
+    #pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const CandInfo c = ci[16 * h + 4 * kh + i];
+                        const int32_t* sbp = (const int32_t*)(smem + c.osb) + m;
+                        const double* twp = (const double*)(smem + L.w + 2 * (c.osb - L.sb)) + m;
+                        const float* twfp = (const float*)(smem + c.osb + (L.wf - L.sb)) + m;   // WF only
+                        const float gT = 2e-6f * fabsf(c.T);
+                        // slow path: n/(n-1) w_a from the pixel's w row
+                        double ca = 0.0;
+                        if constexpr (!FAST) ca = kn * twp[(c.R < 0 ? 0 : c.R) - m];
+                        double sa = 0.0;
+                        uint64_t g = 0;
+                        static_for<NBLK>([&](auto Nc) {
+                            constexpr int nb = Nc;
+                            const int vl = 16 * nb + m;
+                            const int num = __mul24(c.Sa, sbp[16 * nb]) + __mul24(NPX, C[h][nb][i]);
+                            const double w = twp[16 * nb];
+                            uint64_t P;
+                            if constexpr (FAST) {
+                                // ncc > thr <=> num w_b > T; a constant window (w_b = 0 here)
+                                // never passes.  The candidate's own view R passes (its ncc
+                                // is n/(n-1) > thr): its mask bit and its term of the sum
+                                // are taken out once per candidate, not tested per pair
+                                const float x = fmaf((float)num, WF ? twfp[16 * nb] : (float)w, -c.T);
+                                P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
+                                // the lane's bit of P selects the sum's term (no second
+                                // compare), on the integer before the conversion
+                                const int nm = __builtin_amdgcn_inverse_ballot_w64(P) ? num : 0;
+                                g |= __builtin_amdgcn_fcmpf(fabsf(x), gT, 4);                    // olt
+                                sa = fma((double)nm, w, sa);
+                            } else {
+                                const double ncc = (double)num * w * ca;
+                                const bool pass = vl != c.R && ncc > a.thr;
+                                P = __ballot(pass);
+                                g |= __ballot(vl != c.R && fabs(ncc - a.thr) <= kGuard);
+                                sa = fma((double)num, pass ? w : 0.0, sa);
+                            }
+                            if (h == 0) {
+                                pmv[0] = writelane<2 * (i * NBLK + nb)>(pmv[0], (uint32_t)P);
+                                pmv[0] = writelane<2 * (i * NBLK + nb) + 1>(pmv[0], (uint32_t)(P >> 32));
+                            } else {
+                                pmv[1] = writelane<2 * (i * NBLK + nb)>(pmv[1], (uint32_t)P);
+                                pmv[1] = writelane<2 * (i * NBLK + nb) + 1>(pmv[1], (uint32_t)(P >> 32));
+                            }
+                        });
+                        if (h == 0) {
+                            gdv[0] = writelane<2 * i>(gdv[0], (uint32_t)g);
+                            gdv[0] = writelane<2 * i + 1>(gdv[0], (uint32_t)(g >> 32));
                         } else {
-                            const double ncc = (double)num * w * c.ca;
-                            const bool pass = vl != c.R && ncc > a.thr;
-                            P = __ballot(pass);
-                            g |= __ballot(vl != c.R && fabs(ncc - a.thr) <= kGuard);
-                            sa = fma((double)num, pass ? w : 0.0, sa);
+                            gdv[1] = writelane<2 * i>(gdv[1], (uint32_t)g);
+                            gdv[1] = writelane<2 * i + 1>(gdv[1], (uint32_t)(g >> 32));
                         }
-                        pmv = writelane<2 * (i * NBLK + nb)>(pmv, (uint32_t)P);
-                        pmv = writelane<2 * (i * NBLK + nb) + 1>(pmv, (uint32_t)(P >> 32));
-                    });
-                    gdv = writelane<2 * i>(gdv, (uint32_t)g);
-                    gdv = writelane<2 * i + 1>(gdv, (uint32_t)(g >> 32));
-                    sacc[i] = sa;
+                        sacc[h][i] = sa;
+                    }
                 });
-                if (lane < 2 * 4 * NBLK) wp->pm[lane] = pmv;
-                if (lane < 8) wp->gd[lane] = gdv;
-                if (a.avg != nullptr) {
-                    const double mine = row_sum16_x4(sacc, m);
-                    if (m < 4) wp->wsum[4 * kh + m] = mine;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                if (kh == 0 && valid) {
-                    // candidate m = 4 j + i: 16 bits j of ballot (i, nb) -> bits 16 nb of its mask
-                    const int j = m >> 2, i = m & 3;
-                    const uint16_t* pm16 = (const uint16_t*)wp->pm;
+                // owner lane c = 4 j + i (row 0) of each block's candidate c: its mask
+                // bits, guard bits and sum from the lanes that hold them (crossbar
+                // permutes, no LDS storage)
+                const int jj = m >> 2, ii = m & 3;
+    #pragma unroll
+                for (int h = 0; h < 2; ++h) {
                     uint64_t mk = 0;
     #pragma unroll
-                    for (int nb = 0; nb < NBLK; ++nb) mk |= (uint64_t)pm16[4 * (i * NBLK + nb) + j] << (16 * nb);
-                    // the reference view itself is no V entry (MVS2.py:66-67)
-                    const uint64_t self = (mk >> R) & 1ull;
-                    mk &= ~(1ull << R);
-                    const uint32_t gg = ((const uint16_t*)wp->gd)[4 * i + j];
-                    const int cnt = __popcll(mk);
-                    const int64_t idx = e.x;
-                    a.mask[idx] = mk;
-                    a.count[idx] = cnt;
-                    if (a.avg) {
-                        // its own term num_RR w_a = D_a w_a = sqrt(D_a) = 1 / w_a (to the
-                        // rsq + Newton accuracy of w_a, 4e-15) leaves the sum
-                        double inv = __builtin_amdgcn_rcp(my_wa);
-                        inv = inv * (2.0 - my_wa * inv);
-                        const double sum = self ? wp->wsum[m] - inv : wp->wsum[m];
-                        a.avg[idx] = cnt ? sum * my_ca * s_recip[cnt] : 0.0;
+                    for (int nb = 0; nb < NBLK; ++nb) {
+                        const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (2 * (ii * NBLK + nb) + (jj >> 1)), (int)pmv[h]);
+                        mk |= (uint64_t)((d >> (16 * (jj & 1))) & 0xffffu) << (16 * nb);
                     }
-                    if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
+                    const uint32_t gw = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (2 * ii + (jj >> 1)), (int)gdv[h]);
+                    const bool gg = ((gw >> (16 * (jj & 1))) & 0xffffu) != 0u;
+                    double mine = 0.0;
+                    if (a.avg != nullptr) {
+                        const double rs = row_sum16_x4(sacc[h], m);
+                        const int src = 4 * (16 * jj + ii);   // lane 16 j + i holds candidate 4 j + i's sum
+                        const unsigned long long rb64 = __double_as_longlong(rs);
+                        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)rb64);
+                        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(rb64 >> 32));
+                        mine = __longlong_as_double(((unsigned long long)hi << 32) | lo);
+                    }
+                    if (kh == 0 && valid[h]) {
+                        // the reference view itself is no V entry (MVS2.py:66-67)
+                        const uint64_t self = (mk >> Rv[h]) & 1ull;
+                        mk &= ~(1ull << Rv[h]);
+                        const int cnt = __popcll(mk);
+                        const int64_t idx = e[h].x;
+                        a.mask[idx] = mk;
+                        a.count[idx] = cnt;
+                        if (a.avg) {
+                            // its own term num_RR w_a = D_a w_a = sqrt(D_a) = 1 / w_a (to
+                            // the rsq + Newton accuracy of w_a, 4e-15) leaves the sum
+                            double inv = __builtin_amdgcn_rcp(my_wa[h]);
+                            inv = inv * (2.0 - my_wa[h] * inv);
+                            const double sum = self ? mine - inv : mine;
+                            a.avg[idx] = cnt ? sum * my_ca[h] * s_recip[cnt] : 0.0;
+                        }
+                        if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
+                    }
                 }
             }
             STAMP(t3);
@@ -1183,12 +1271,6 @@ __host__ __device__ constexpr int v_static_lds() {
 // __syncthreads would wait for them: vmcnt(0)).
 DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// x through an opaque copy: what is computed from it is computed where it is
-// used, not hoisted out of loops into long-lived registers
-DEV int opaque(int x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
 
 // byte masks of a window of NB bytes starting at byte b0 over the 4 dwords
 // from dword b0 >> 2
@@ -2017,7 +2099,7 @@ int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipSt
         // the largest table is sized for V = 16 NBLK; every V of this NBLK fits in it
         const int lds = mma_layout<WID, NBLK>(16 * NBLK).total;
         const int used = mma_layout<WID, NBLK>(sc->V).total;
-        if (fabs(a->thr) >= 0.01) {
+        if (a->thr >= 0.01) {   // FAST: T > 0 (a constant window's w = 0 can never pass)
             if (set_dyn_lds_once((const void*)k_score_mma<WID, NBLK, true>, attr_fast, lds) != 0) return -1;
             hipLaunchKernelGGL((k_score_mma<WID, NBLK, true>), dim3(kMmaGrid), dim3(kMmaThreads), used, s, *sc, *a,
                                *t, (const int4*)t->items, (const int2*)t->sorted);

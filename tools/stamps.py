@@ -13,8 +13,9 @@ faulthandler.dump_traceback_later(150, exit=True)   # a stuck run names its line
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-os.environ["MVS_LIB"] = os.path.join(REPO, "simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd",
-                                     "libmvs_amd_stamps.so")
+os.environ["MVS_LIB"] = os.environ.get("STAMPS_LIB") or os.path.join(
+    REPO, "simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd", "libmvs_amd_stamps.so")
+print("library", os.path.basename(os.environ["MVS_LIB"]))
 import bench  # noqa: E402
 
 wid = int(sys.argv[1]) if len(sys.argv) > 1 else 5
