@@ -37,6 +37,8 @@ def build(force=False, verbose=False, stamps=False, asan=False):
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
     if stamps:
         cmd.append("-DMVS_STAMPS")
+        # diagnostic A/B switches for the stamps build, e.g. MVS_STAMPS_DEFS=MVS_DIAG_NOSTORE
+        cmd += [f"-D{d}" for d in os.environ.get("MVS_STAMPS_DEFS", "").split()]
     if asan:
         # the host code only (the engine's commit, seeding, filter, sort
         # bookkeeping, C-ABI checks); device code is never sanitized here

@@ -515,6 +515,7 @@ constexpr int kGroupViews = MVS_GROUP_VIEWS;   // views per view group (V > 64):
 constexpr int kMmaChunk = MVS_MMA_CHUNK;       // candidates per work item, V <= 64 (k_tile_scan: <= 1024)
 constexpr int kGroupChunk = MVS_GROUP_CHUNK;   // candidates per work item, V > 64 (reference windows staged)
 constexpr int kMmaGrid = 256;         // one workgroup per CU; the queue balances
+constexpr int kSortBins = MVS_TILE_H / 2;   // k_score_mma sorts an item's candidates by row pair
 
 template <int WID>
 struct MmaGeom {
@@ -534,6 +535,23 @@ struct MmaGeom {
 DEV int opaque(int x) {
     asm volatile("" : "+v"(x));
     return x;
+}
+
+// acc += num * w in the lanes of P only (binary64): EXEC narrowed to P for
+// the conversion and the fma, restored after -- two vector instructions, no
+// select of the term (the compiler's form of the select costs four)
+DEV double fma_f64_lanes(double acc, int num, double w, uint64_t P) {
+    double t;
+    uint64_t save;
+    asm volatile(
+        "s_and_saveexec_b64 %[save], %[p]\n\t"
+        "v_cvt_f64_i32 %[t], %[num]\n\t"
+        "v_fma_f64 %[acc], %[t], %[w], %[acc]\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [acc] "+v"(acc), [t] "=&v"(t), [save] "=&s"(save)
+        : [num] "v"(num), [w] "v"(w), [p] "s"(P)
+        : "exec", "scc");
+    return acc;
 }
 
 // 4-bit column mask -> byte mask
@@ -571,20 +589,31 @@ __constant__ constexpr RecipTable c_recip{};
 //      k_score_fix (numpy-order ctNcc).  avg_ncc_score = n/(n-1) w_a
 //      sum(num w_b) / cnt in binary64.
 // ---------------------------------------------------------------------------
+#ifdef MVS_DIAG_NOSTORE
+#define MVS_DIAG_STORE_OK(idx) ((idx) == -7)
+#else
+#define MVS_DIAG_STORE_OK(idx) true
+#endif
 #ifdef MVS_STAMPS
 // diagnostic build only: per-workgroup cycle sums of the scorer's phases
 // (slot 0 items, 1 staging + barrier, 2 moments, 3 candidates, 4 wave 0's own
 // candidate time, 5 wave 0's M-blocks), read by mvs_read_stamps
-__device__ unsigned long long g_stamps[4096 * 8];
+__device__ unsigned long long g_stamps[4096 * 16];
 #define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, val) \
-    do { if (threadIdx.x == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 8 + (slot)], (unsigned long long)(val)); } while (0)
+    do { if (threadIdx.x == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
 #define STAMP_ADD_W0(slot, val) \
-    do { if ((threadIdx.x & 1023) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 8 + (slot)], (unsigned long long)(val)); } while (0)
+    do { if ((threadIdx.x & 1023) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
+// any lane / one lane per wave
+#define STAMP_ADD_ANY(slot, val) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val))
+#define STAMP_ADD_LANE0(slot, val) \
+    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
 #else
 #define STAMP(var)
 #define STAMP_ADD(slot, val)
 #define STAMP_ADD_W0(slot, val)
+#define STAMP_ADD_ANY(slot, val)
+#define STAMP_ADD_LANE0(slot, val)
 #endif
 
 // a candidate's constants in phase 3 (per wave, 32 slots: the two M-blocks
@@ -631,7 +660,7 @@ __host__ __device__ constexpr MmaLds mma_lds(int V) {
 template <int WID, int NBLK, bool DB>
 __host__ __device__ constexpr int mma_static_lds() {
     return (DB ? 2 * (16 * NBLK * MmaGeom<WID>::VS + kMmaChunk * 8) : 64) + 8 + 4 + 65 * 8 + 64 +
-           MVS_TILE_H * kMmaWaves * 3;   // the row sort's counts and offsets
+           kSortBins * kMmaWaves * 3;   // the row sort's counts and offsets
 }
 
 // what fits in 160 KiB beside the rest at this NBLK (1 workgroup of 16 waves
@@ -689,16 +718,23 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB], s_reg1[RB];
     __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[CB];
     __shared__ int s_ids[2];
+    __shared__ int s_simd_n[4];
     __shared__ int s_V;
     __shared__ double s_recip[65];
     // the item's candidates are reordered by pixel row inside the tile (a
     // counting sort in LDS): per (wave, row) counts and destination offsets
-    __shared__ __attribute__((aligned(16))) uint8_t s_rcnt[MVS_TILE_H][kMmaWaves];
-    __shared__ __attribute__((aligned(16))) int16_t s_roff[MVS_TILE_H][kMmaWaves];
+#ifdef MVS_STAMPS
+    __shared__ unsigned s_maxown;
+    if (threadIdx.x == 0) s_maxown = 0;
+#endif
+    __shared__ __attribute__((aligned(16))) uint8_t s_rcnt[kSortBins][kMmaWaves];
+    __shared__ __attribute__((aligned(16))) int16_t s_roff[kSortBins][kMmaWaves];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int V = sc.V;
     const int npiece = V * RPV * 2;
+    // k / V as umulhi(k, ceil(2^32 / V)): exact for k V < 2^32 (uniform, once)
+    const uint32_t vmagic = __builtin_amdgcn_readfirstlane(0xffffffffu / (uint32_t)V + 1u);
     if (tid <= 64) s_recip[tid] = c_recip.r[tid];
     if (tid == 0) s_V = V;
     const MmaLds L = mma_layout<WID, NBLK>(V);
@@ -760,7 +796,18 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
         s_ids[0] = atomicAdd(head, 1);
         s_ids[1] = atomicAdd(head, 1);
     }
+    // The 16 waves sit 4 to a SIMD, which shares its issue among them: work is
+    // split by SIMD (virtual wave vw = 4 SIMD + rank on it) where it does not
+    // divide evenly over the waves.  vw = wave unless every SIMD holds 4 waves.
+    if (tid < 4) s_simd_n[tid] = 0;
     __syncthreads();
+    const int simd = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);   // HW_ID.SIMD_ID
+    int srank = 0;
+    if (lane == 0) srank = atomicAdd(&s_simd_n[simd & 3], 1);
+    srank = __builtin_amdgcn_readfirstlane(srank);
+    __syncthreads();
+    const bool simd_ok = s_simd_n[0] == 4 && s_simd_n[1] == 4 && s_simd_n[2] == 4 && s_simd_n[3] == 4;
+    const int vw = __builtin_amdgcn_readfirstlane(simd_ok ? 4 * (simd & 3) + srank : wave);
     int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
     int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
     if (cur >= n_units) return;
@@ -791,34 +838,39 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             // thread -> (row, view) maps of phase 2, from a V read after the
             // barrier (not hoisted: no registers held across phase 3)
             const int Vl = s_V;
-            const int h_rho0 = tid / Vl, h_v0 = tid - h_rho0 * Vl;
-            const bool m2 = tid < Vl * 16;
-            // sort of the candidates by pixel row (rrel), stable: thread k holds
-            // candidate k; its rank among the wave's candidates of its row now,
-            // the destination after the offsets are known (phase 2 barriers)
+            // tasks split into four contiguous SIMD segments (vw = 4 SIMD + rank):
+            // each SIMD issues a quarter of them whatever the task count
+            const int ploc = (vw & 3) * 64 + lane, pseg = vw >> 2;
+            const int hq = (Vl * ROWS + 3) >> 2, vq = (Vl * 16 + 3) >> 2;   // per-SIMD quotas
+            const int vtask = pseg * vq + ploc;
+            const int h_rho0 = (int)__umulhi((uint32_t)vtask, vmagic), h_v0 = vtask - h_rho0 * Vl;   // vertical: (column, view)
+            const bool m2 = ploc < vq && vtask < Vl * 16;
+            // sort of the candidates by pixel row pair (rrel >> 1: a K-step's two
+            // region rows), stable: thread k holds candidate k; its rank among
+            // the wave's candidates of its row pair now, the destination after
+            // the offsets are known (phase 2 barriers)
             int2 my_c = make_int2(0, 0);
-            int my_row = MVS_TILE_H, my_rank = 0;
+            int my_row = kSortBins, my_rank = 0;
             if (tid < nc) {
                 my_c = ((const int2*)cand_buf(buf))[tid];
-                my_row = (my_c.y >> 4) & 7;
+                my_row = (my_c.y >> 5) & 3;
             }
-            int my_cnt = 0;   // lane y < 8: the wave's count of row y
-            static_for<MVS_TILE_H>([&](auto Yc) {
+            int my_cnt = 0;   // lane y < kSortBins: the wave's count of bin y
+            static_for<kSortBins>([&](auto Yc) {
                 constexpr int y = Yc;
                 const uint64_t bm = __ballot(my_row == y);
                 if (my_row == y) my_rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
                 my_cnt = writelane<y>((uint32_t)my_cnt, (uint32_t)__popcll(bm));
             });
-            if (lane < MVS_TILE_H) s_rcnt[lane][wave] = (uint8_t)my_cnt;
+            if (lane < kSortBins) s_rcnt[lane][wave] = (uint8_t)my_cnt;
             // ---- 2. S_b and w of every view at the tile's pixels ----
             // horizontal sums of each region row on the unsigned bytes g = s + 128
             // (the moments are shift invariant): prefix sums by v_sad_u8 and
             // v_dot4_u32_u8, packed as (sum g^2) << 12 | sum g
-    #pragma unroll
-            for (int j = 0; j < HT; ++j) {
-                if (tid + j * kMmaThreads < V * ROWS) {
-                    const int k = tid + j * kMmaThreads;
-                    const int rho = j ? k / Vl : h_rho0, v = j ? k - rho * Vl : h_v0;
+            for (int j = 0; ploc + 256 * j < hq; ++j) {
+                const int k = pseg * hq + ploc + 256 * j;
+                if (k < V * ROWS) {
+                    const int rho = (int)__umulhi((uint32_t)k, vmagic), v = k - rho * Vl;
                     const uint4 lo = *(const uint4*)(reg + v * VS + rho * 32);
                     const uint4 hi = *(const uint4*)(reg + v * VS + rho * 32 + 16);
                     const uint32_t d[8] = {lo.x ^ 0x80808080u, lo.y ^ 0x80808080u, lo.z ^ 0x80808080u,
@@ -850,7 +902,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             // destination offsets of the row sort: row y's candidates start after
             // every candidate of rows < y, then by wave (lane y of the last wave:
             // the row's 16 wave counts in one read, prefix sums in registers)
-            if (wave == kMmaWaves - 1 && lane < MVS_TILE_H) {
+            if (wave == kMmaWaves - 1 && lane < kSortBins) {
                 const uint4 q4 = *(const uint4*)&s_rcnt[lane][0];
                 const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
                 int pre[kMmaWaves];
@@ -862,7 +914,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 }
                 int ex = tot;
     #pragma unroll
-                for (int off = 1; off < MVS_TILE_H; off <<= 1) {
+                for (int off = 1; off < kSortBins; off <<= 1) {
                     const int yv = __shfl_up(ex, off, 64);
                     if (lane >= off) ex += yv;
                 }
@@ -948,120 +1000,51 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 if (tid == 0) pend = atomicAdd(head, 1);
             }
     
-            // ---- 3. + 4. the candidates: a wave takes units of two M-blocks of
-            // 16 (32 consecutive candidates of the row-sorted list), which share
-            // their K-steps and B operands and give the epilogue two
-            // independent chains ----
+            // ---- 3. + 4. the candidates: units of two M-blocks of 16 (32
+            // consecutive candidates of the row-sorted list), which share their
+            // K-steps and B operands and give the epilogue two independent
+            // chains.  The SIMDs share the issue of their waves, so the blocks
+            // are split into four contiguous SIMD segments of equal size; a
+            // segment's waves take its units (the last one may be a single
+            // block) ----
             const int nblk = (nc + 15) >> 4;
-            const int nunit = (nblk + 1) >> 1;
+            const int sg = vw >> 2, sr = vw & 3;           // SIMD segment, wave rank in it
+            const int seg_b = (nblk * sg) >> 2, seg_e = (nblk * (sg + 1)) >> 2;
     #ifdef MVS_STAMPS
             unsigned long long w0blk = 0;
     #endif
-            for (int u = wave; u < nunit; u += kMmaWaves) {
+            for (int fb = seg_b + 2 * sr; fb < seg_e; fb += 8) {
+              const int nh = min(2, seg_e - fb);
     #ifdef MVS_STAMPS
-                w0blk += 2;
+              w0blk += nh;
     #endif
+              auto unit = [&](auto nhc) {
+                constexpr int NH = decltype(nhc)::value;
                 // lane constants recomputed per unit (hoisted, they would hold
                 // registers through phase 2)
                 const int ol = opaque(lane);
                 const int m = ol & 15, kh = ol >> 4;
-                int2 e[2];
-                bool valid[2];
-                int qrel[2], rrel[2], Rv[2];
+                int2 e[NH];
+                bool valid[NH];
+                int qrel[NH], rrel[NH], Rv[NH];
     #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int kk = u * 32 + 16 * h + m;
+                for (int h = 0; h < NH; ++h) {
+                    const int kk = (fb + h) * 16 + m;
                     valid[h] = kk < nc;
                     e[h] = valid[h] ? cand[kk] : make_int2(-1, 0);
                     qrel[h] = e[h].y & 15;
                     rrel[h] = (e[h].y >> 4) & 7;
                     Rv[h] = e[h].y >> 7;
                 }
-                // the unit's candidates are sorted by row: its window rows span
-                // candidate 0's row to the last valid candidate's row + NB - 1
-                const int last = min(31, nc - 1 - u * 32);
-                const int r_lo = __builtin_amdgcn_readlane(rrel[0], 0);
-                const int r_hi = last >= 16 ? __builtin_amdgcn_readlane(rrel[1], last - 16)
-                                            : __builtin_amdgcn_readlane(rrel[0], last);
-                constexpr int KSK = WID + 1;     // K-steps of one row's windows
-                const int s_lo = r_lo >> 1, s_hi = (r_hi + NB - 1) >> 1;
-                const int span = s_hi - s_lo + 1;
-                // A: the reference windows, masked to each candidate's window
-                // columns (this lane's 16 columns) and rows (bit 2s: K-step s holds
-                // a window row of this lane's row parity)
-                uint32_t cm[2][4], rb[2];
-    #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t wm = valid[h] ? (((1u << NB) - 1u) << (qrel[h] + C0)) : 0u;
-                    const uint32_t hm = wm >> (16 * (kh & 1));
-    #pragma unroll
-                    for (int k4 = 0; k4 < 4; ++k4) cm[h][k4] = byte_mask((hm >> (4 * k4)) & 15u);
-                    rb[h] = valid[h] ? (((1u << NB) - 1u) << rrel[h]) >> (kh >> 1) : 0u;
-                }
-                const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
-                v4i C[2][NBLK];
-    #pragma unroll
-                for (int h = 0; h < 2; ++h)
-    #pragma unroll
-                    for (int nb = 0; nb < NBLK; ++nb) C[h][nb] = (v4i){0, 0, 0, 0};
-                // NST K-steps from sb; steps below sd are done (their A rows read zeros)
-                auto kpass = [&](auto nstc, int sb, int sd) {
-                    constexpr int NST = decltype(nstc)::value;
-                    uint32_t rbp[2];
-                    const uint8_t* aptr[2];
-    #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        rbp[h] = (rb[h] & ~((1u << (2 * sd)) - 1u)) >> (2 * sb);
-                        aptr[h] = reg + Rv[h] * VS + lofs + 64 * sb;
-                    }
-                    const uint8_t* bptr[NBLK];
-    #pragma unroll
-                    for (int nb = 0; nb < NBLK; ++nb) bptr[nb] = reg + min(16 * nb + m, V - 1) * VS + lofs + 64 * sb;
-                    // operands of step st + 1 load while step st's MFMAs run; the
-                    // schedule barrier keeps the compiler from hoisting more loads
-                    // (their registers would spill)
-                    uint4 av[2][2], bv[2][NBLK];
-                    auto load = [&](int st, int slot) {
-    #pragma unroll
-                        for (int h = 0; h < 2; ++h)
-                            // rows outside the window read 16 zero bytes: an address
-                            // select instead of a branch around the load
-                            av[slot][h] = *(const uint4*)(((rbp[h] >> (2 * st)) & 1u) ? aptr[h] + 64 * st : zrow);
-    #pragma unroll
-                        for (int nb = 0; nb < NBLK; ++nb) bv[slot][nb] = *(const uint4*)(bptr[nb] + 64 * st);
-                    };
-                    load(0, 0);
-    #pragma unroll
-                    for (int st = 0; st < NST; ++st) {
-                        const int cur = st & 1;
-                        if (st + 1 < NST) load(st + 1, cur ^ 1);
-                        v4i A[2];
-    #pragma unroll
-                        for (int h = 0; h < 2; ++h)
-                            A[h] = (v4i){(int)(av[cur][h].x & cm[h][0]), (int)(av[cur][h].y & cm[h][1]),
-                                         (int)(av[cur][h].z & cm[h][2]), (int)(av[cur][h].w & cm[h][3])};
-    #pragma unroll
-                        for (int nb = 0; nb < NBLK; ++nb) {
-                            const v4i B = {(int)bv[cur][nb].x, (int)bv[cur][nb].y, (int)bv[cur][nb].z, (int)bv[cur][nb].w};
-                            C[0][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B, C[0][nb], 0, 0, 0);
-                            C[1][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B, C[1][nb], 0, 0, 0);
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                };
-                if (span <= KSK) {
-                    kpass(std::integral_constant<int, KSK>{}, min(s_lo, KS - KSK), 0);
-                } else if (span == KSK + 1) {
-                    kpass(std::integral_constant<int, KSK + 1>{}, min(s_lo, KS - KSK - 1), 0);
-                } else {
-                    for (int sd = s_lo; sd <= s_hi; sd += KSK) kpass(std::integral_constant<int, KSK>{}, min(sd, KS - KSK), sd);
-                }
                 // the candidates' constants (row 0 of the wave computes them for
-                // both blocks), shared through LDS
-                double my_ca[2] = {0.0, 0.0}, my_wa[2] = {0.0, 0.0};
+                // both blocks, before the K-loop: they do not depend on it), shared
+                // through LDS
+                double my_wa[NH];
+    #pragma unroll
+                for (int h = 0; h < NH; ++h) my_wa[h] = 0.0;
                 if (kh == 0) {
     #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
+                    for (int h = 0; h < NH; ++h) {
                         CandInfo c;
                         const int px = e[h].y & 127;          // rrel * 16 + qrel
                         const int o = px * VP + Rv[h];
@@ -1073,19 +1056,100 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         // well inside the guard band); else the decision is on ncc
                         c.T = FAST ? (valid[h] ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf("")) : 0.0f;
                         ci[16 * h + m] = c;
-                        my_ca[h] = kn * wa;
                         my_wa[h] = wa;
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+                // the unit's candidates are sorted by row pair: its window rows lie
+                // in candidate 0's pair to the last valid candidate's pair + NB - 1
+                const int last = min(16 * NH - 1, nc - 1 - fb * 16);
+                const int r_lo = __builtin_amdgcn_readlane(rrel[0], 0) & ~1;
+                const int r_hi = (last >= 16 ? __builtin_amdgcn_readlane(rrel[NH - 1], last - 16)
+                                             : __builtin_amdgcn_readlane(rrel[0], last)) | 1;
+                constexpr int KSK = WID + 1;     // K-steps of one row's windows
+                const int s_lo = r_lo >> 1, s_hi = (r_hi + NB - 1) >> 1;
+                const int span = s_hi - s_lo + 1;
+                // A: the reference windows, masked to each candidate's window
+                // columns (this lane's 16 columns) and rows (bit 2s: K-step s holds
+                // a window row of this lane's row parity)
+                uint32_t cm[NH][4], rb[NH];
+    #pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    const uint32_t wm = valid[h] ? (((1u << NB) - 1u) << (qrel[h] + C0)) : 0u;
+                    const uint32_t hm = wm >> (16 * (kh & 1));
+    #pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) cm[h][k4] = byte_mask((hm >> (4 * k4)) & 15u);
+                    rb[h] = valid[h] ? (((1u << NB) - 1u) << rrel[h]) >> (kh >> 1) : 0u;
+                }
+                const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
+                v4i C[NH][NBLK];
+    #pragma unroll
+                for (int h = 0; h < NH; ++h)
+    #pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) C[h][nb] = (v4i){0, 0, 0, 0};
+                // NST K-steps from sb; steps below sd are done (their A rows read zeros)
+                auto kpass = [&](auto nstc, int sb, int sd) {
+                    constexpr int NST = decltype(nstc)::value;
+                    uint32_t rbp[NH];
+                    const uint8_t* aptr[NH];
+    #pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        rbp[h] = (rb[h] & ~((1u << (2 * sd)) - 1u)) >> (2 * sb);
+                        aptr[h] = reg + Rv[h] * VS + lofs + 64 * sb;
+                    }
+                    const uint8_t* bptr[NBLK];
+    #pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) bptr[nb] = reg + min(16 * nb + m, V - 1) * VS + lofs + 64 * sb;
+                    // operands of step st + 1 load while step st's MFMAs run; the
+                    // schedule barrier keeps the compiler from hoisting more loads
+                    // (their registers would spill)
+                    uint4 av[2][NH], bv[2][NBLK];
+                    auto load = [&](int st, int slot) {
+    #pragma unroll
+                        for (int h = 0; h < NH; ++h)
+                            // rows outside the window read 16 zero bytes: an address
+                            // select instead of a branch around the load
+                            av[slot][h] = *(const uint4*)(((rbp[h] >> (2 * st)) & 1u) ? aptr[h] + 64 * st : zrow);
+    #pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) bv[slot][nb] = *(const uint4*)(bptr[nb] + 64 * st);
+                    };
+                    load(0, 0);
+    #pragma unroll
+                    for (int st = 0; st < NST; ++st) {
+                        const int cur = st & 1;
+                        if (st + 1 < NST) load(st + 1, cur ^ 1);
+                        v4i A[NH];
+    #pragma unroll
+                        for (int h = 0; h < NH; ++h)
+                            A[h] = (v4i){(int)(av[cur][h].x & cm[h][0]), (int)(av[cur][h].y & cm[h][1]),
+                                         (int)(av[cur][h].z & cm[h][2]), (int)(av[cur][h].w & cm[h][3])};
+    #pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) {
+                            const v4i B = {(int)bv[cur][nb].x, (int)bv[cur][nb].y, (int)bv[cur][nb].z, (int)bv[cur][nb].w};
+    #pragma unroll
+                            for (int h = 0; h < NH; ++h)
+                                C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[h], B, C[h][nb], 0, 0, 0);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                };
+                if (span <= KSK) {
+                    kpass(std::integral_constant<int, KSK>{}, min(s_lo, KS - KSK), 0);
+                } else if (span == KSK + 1) {
+                    kpass(std::integral_constant<int, KSK + 1>{}, min(s_lo, KS - KSK - 1), 0);
+                } else {
+                    for (int sd = s_lo; sd <= s_hi; sd += KSK) kpass(std::integral_constant<int, KSK>{}, min(sd, KS - KSK), sd);
+                }
                 // lane (kh, m) holds C[h][nb][i] = block h's candidate 4 kh + i, view 16 nb + m
-                uint32_t pmv[2] = {0u, 0u}, gdv[2] = {0u, 0u};
-                double sacc[2][4];
+                uint32_t pmv[NH], gdv[NH];
+    #pragma unroll
+                for (int h = 0; h < NH; ++h) pmv[h] = gdv[h] = 0u;
+                double sacc[NH][4];
                 static_for<4>([&](auto Ic) {
                     constexpr int i = Ic;
     #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
+                    for (int h = 0; h < NH; ++h) {
                         const CandInfo c = ci[16 * h + 4 * kh + i];
                         const int32_t* sbp = (const int32_t*)(smem + c.osb) + m;
                         const double* twp = (const double*)(smem + L.w + 2 * (c.osb - L.sb)) + m;
@@ -1096,6 +1160,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         if constexpr (!FAST) ca = kn * twp[(c.R < 0 ? 0 : c.R) - m];
                         double sa = 0.0;
                         uint64_t g = 0;
+                        float ax[NBLK];   // FAST: the decision values, for the guard test
                         static_for<NBLK>([&](auto Nc) {
                             constexpr int nb = Nc;
                             const int vl = 16 * nb + m;
@@ -1109,11 +1174,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                                 // are taken out once per candidate, not tested per pair
                                 const float x = fmaf((float)num, WF ? twfp[16 * nb] : (float)w, -c.T);
                                 P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
-                                // the lane's bit of P selects the sum's term (no second
-                                // compare), on the integer before the conversion
-                                const int nm = __builtin_amdgcn_inverse_ballot_w64(P) ? num : 0;
-                                g |= __builtin_amdgcn_fcmpf(fabsf(x), gT, 4);                    // olt
-                                sa = fma((double)nm, w, sa);
+                                ax[nb] = x;
+                                // the sum's term in the passing lanes only
+                                sa = fma_f64_lanes(sa, num, w, P);
                             } else {
                                 const double ncc = (double)num * w * ca;
                                 const bool pass = vl != c.R && ncc > a.thr;
@@ -1121,21 +1184,18 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                                 g |= __ballot(vl != c.R && fabs(ncc - a.thr) <= kGuard);
                                 sa = fma((double)num, pass ? w : 0.0, sa);
                             }
-                            if (h == 0) {
-                                pmv[0] = writelane<2 * (i * NBLK + nb)>(pmv[0], (uint32_t)P);
-                                pmv[0] = writelane<2 * (i * NBLK + nb) + 1>(pmv[0], (uint32_t)(P >> 32));
-                            } else {
-                                pmv[1] = writelane<2 * (i * NBLK + nb)>(pmv[1], (uint32_t)P);
-                                pmv[1] = writelane<2 * (i * NBLK + nb) + 1>(pmv[1], (uint32_t)(P >> 32));
-                            }
+                            pmv[h] = writelane<2 * (i * NBLK + nb)>(pmv[h], (uint32_t)P);
+                            pmv[h] = writelane<2 * (i * NBLK + nb) + 1>(pmv[h], (uint32_t)(P >> 32));
                         });
-                        if (h == 0) {
-                            gdv[0] = writelane<2 * i>(gdv[0], (uint32_t)g);
-                            gdv[0] = writelane<2 * i + 1>(gdv[0], (uint32_t)(g >> 32));
-                        } else {
-                            gdv[1] = writelane<2 * i>(gdv[1], (uint32_t)g);
-                            gdv[1] = writelane<2 * i + 1>(gdv[1], (uint32_t)(g >> 32));
+                        if constexpr (FAST) {
+                            // guard band: min over the views of |x| < gT (one compare)
+                            float mn = fabsf(ax[0]);
+    #pragma unroll
+                            for (int nb = 1; nb < NBLK; ++nb) mn = fminf(mn, fabsf(ax[nb]));
+                            g = __builtin_amdgcn_fcmpf(mn, gT, 4);                               // olt
                         }
+                        gdv[h] = writelane<2 * i>(gdv[h], (uint32_t)g);
+                        gdv[h] = writelane<2 * i + 1>(gdv[h], (uint32_t)(g >> 32));
                         sacc[h][i] = sa;
                     }
                 });
@@ -1144,7 +1204,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 // permutes, no LDS storage)
                 const int jj = m >> 2, ii = m & 3;
     #pragma unroll
-                for (int h = 0; h < 2; ++h) {
+                for (int h = 0; h < NH; ++h) {
                     uint64_t mk = 0;
     #pragma unroll
                     for (int nb = 0; nb < NBLK; ++nb) {
@@ -1168,21 +1228,43 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         mk &= ~(1ull << Rv[h]);
                         const int cnt = __popcll(mk);
                         const int64_t idx = e[h].x;
+    #ifdef MVS_DIAG_NOSTORE
+                        // diagnostic build: the outputs computed, not stored
+                        if (idx == -7) {
+    #else
+                        {
+    #endif
                         a.mask[idx] = mk;
                         a.count[idx] = cnt;
-                        if (a.avg) {
+                        }
+                        if (a.avg && MVS_DIAG_STORE_OK(idx)) {
                             // its own term num_RR w_a = D_a w_a = sqrt(D_a) = 1 / w_a (to
                             // the rsq + Newton accuracy of w_a, 4e-15) leaves the sum
                             double inv = __builtin_amdgcn_rcp(my_wa[h]);
                             inv = inv * (2.0 - my_wa[h] * inv);
                             const double sum = self ? mine - inv : mine;
-                            a.avg[idx] = cnt ? sum * my_ca[h] * s_recip[cnt] : 0.0;
+                            a.avg[idx] = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
                         }
-                        if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
+                        if (gg) {
+                            t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
+                            STAMP_ADD_ANY(11, 1);
+                        }
                     }
                 }
+    #ifdef MVS_STAMPS
+                STAMP_ADD_LANE0(12, span > KSK ? 1 : 0);
+                STAMP_ADD_LANE0(13, 1);
+    #endif
+              };
+              if (nh == 2) unit(std::integral_constant<int, 2>{});
+              else unit(std::integral_constant<int, 1>{});
             }
             STAMP(t3);
+    #ifdef MVS_STAMPS
+            // slowest wave's own phase-3 time (per item: slot 9), every wave's (10)
+            if (lane == 0) atomicMax(&s_maxown, (unsigned)(t3 - t2));
+            STAMP_ADD_LANE0(10, t3 - t2);
+    #endif
             __syncthreads();
             STAMP(t4);
             STAMP_ADD(0, 1);
@@ -1193,6 +1275,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             STAMP_ADD_W0(5, w0blk);
             STAMP_ADD(6, t1a - t1);
             STAMP_ADD(7, t1b - t1a);
+            STAMP_ADD_W0(8, t4 - t3);
+    #ifdef MVS_STAMPS
+            if (tid == 0) {
+                STAMP_ADD_ANY(9, s_maxown);
+                s_maxown = 0;
+            }
+    #endif
         if (nx1 >= n_units) return false;
         if constexpr (!DB) stage(dnx1, std::integral_constant<int, 0>{});   // the buffer is free now; lands by the next barrier
         cur = nx1;

@@ -34,13 +34,13 @@ ctx = pkg.MvsContext(rgb, K, R, t)
 print("context ready", flush=True)
 lib = pkg._lib.load()
 lib.mvs_read_stamps.argtypes = [ctypes.c_void_p]
-buf = np.zeros(4096 * 8, np.uint64)
+buf = np.zeros(4096 * 16, np.uint64)
 ctx.score(c, ref, 0.7, wid)
 lib.mvs_read_stamps(buf.ctypes.data)
 before = buf.copy()
 ctx.score(c, ref, 0.7, wid)
 lib.mvs_read_stamps(buf.ctypes.data)
-d = (buf - before).reshape(4096, 8).astype(np.float64)
+d = (buf - before).reshape(4096, 16).astype(np.float64)
 items = d[:, 0]
 act = items > 0
 tot = items.sum()
@@ -55,5 +55,10 @@ for k, name in labels:
 if scene != "ring256":
   print(f"  wave 0: {d[act, 4].sum() / tot:9.0f} cycles of own candidate work per item, "
       f"{d[act, 5].sum() / tot:.2f} M-blocks per item -> {d[act, 4].sum() / max(d[act, 5].sum(), 1):.0f} cycles per M-block")
+if scene != "ring256" and d[act, 13].sum() > 0:
+    print(f"  wave 0 final-barrier wait {d[act, 8].sum() / tot:9.0f} cycles per item; own phase-3 time: "
+          f"slowest wave {d[act, 9].sum() / tot:9.0f}, mean of the 16 waves {d[act, 10].sum() / tot / 16:9.0f}")
+    print(f"  units {d[act, 13].sum() / tot:.2f} per item, {d[act, 12].sum() / max(d[act, 13].sum(), 1) * 100:.1f} % span > KSK; "
+          f"fix-list appends {d[act, 11].sum() / tot:.2f} per item")
 per_wg = d[act, 1] + d[act, 2] + d[act, 3]
 print(f"  per workgroup {per_wg.mean():.0f} cycles (max {per_wg.max():.0f})")
