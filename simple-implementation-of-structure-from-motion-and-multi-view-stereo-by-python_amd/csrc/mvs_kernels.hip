@@ -709,7 +709,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     constexpr bool WF = mma_wf<WID, NBLK>(), DB = mma_db<WID, NBLK>();
     constexpr int RPV = VS / 32;                          // region rows per view incl. the pad row
     constexpr int PF = (VP * RPV * 2 + kMmaThreads - 1) / kMmaThreads;   // 16-B pieces per thread
-    constexpr int HT = (VP * ROWS + kMmaThreads - 1) / kMmaThreads;       // horizontal-sum tasks per thread
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // DB: the two region and candidate buffers are distinct LDS objects, so
     // that the compiler sees that reads of one do not alias the LDS-DMA into
@@ -750,7 +749,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     const float tqf = (float)(a.thr / kn);
     const int n_units = t.item_off[t.ntiles];
     int32_t* head = &t.tile_count[t.ntiles];
-    const int m = lane & 15, kh = lane >> 4;
 
     // The region of an item (gv rows, signed bytes) goes to LDS by LDS-DMA
     // (global_load_lds_dwordx4: 64 lanes x 16 B land contiguously), 32 B per
@@ -1089,8 +1087,11 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     #pragma unroll
                     for (int nb = 0; nb < NBLK; ++nb) C[h][nb] = (v4i){0, 0, 0, 0};
                 // NST K-steps from sb; steps below sd are done (their A rows read zeros)
-                auto kpass = [&](auto nstc, int sb, int sd) {
+                // steps [SAFE_LO, SAFE_HI] of the pass hold window rows of every
+                // candidate of the unit (no row test there)
+                auto kpass = [&](auto nstc, auto safe_lo_c, auto safe_hi_c, int sb, int sd) {
                     constexpr int NST = decltype(nstc)::value;
+                    constexpr int SAFE_LO = decltype(safe_lo_c)::value, SAFE_HI = decltype(safe_hi_c)::value;
                     uint32_t rbp[NH];
                     const uint8_t* aptr[NH];
     #pragma unroll
@@ -1110,7 +1111,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         for (int h = 0; h < NH; ++h)
                             // rows outside the window read 16 zero bytes: an address
                             // select instead of a branch around the load
-                            av[slot][h] = *(const uint4*)(((rbp[h] >> (2 * st)) & 1u) ? aptr[h] + 64 * st : zrow);
+                            av[slot][h] = *(const uint4*)((st >= SAFE_LO && st <= SAFE_HI) || ((rbp[h] >> (2 * st)) & 1u)
+                                                              ? aptr[h] + 64 * st : zrow);
     #pragma unroll
                         for (int nb = 0; nb < NBLK; ++nb) bv[slot][nb] = *(const uint4*)(bptr[nb] + 64 * st);
                     };
@@ -1134,12 +1136,19 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 };
+                // one row pair (span KSK, from s_lo <= KS - KSK): steps 1 .. KSK-2
+                // hold rows of every window; two (span KSK+1): steps 2 .. KSK-2
+                using I = std::integral_constant<int, 0>;
                 if (span <= KSK) {
-                    kpass(std::integral_constant<int, KSK>{}, min(s_lo, KS - KSK), 0);
+                    kpass(std::integral_constant<int, KSK>{}, std::integral_constant<int, 1>{},
+                          std::integral_constant<int, KSK - 2>{}, min(s_lo, KS - KSK), 0);
                 } else if (span == KSK + 1) {
-                    kpass(std::integral_constant<int, KSK + 1>{}, min(s_lo, KS - KSK - 1), 0);
+                    kpass(std::integral_constant<int, KSK + 1>{}, std::integral_constant<int, 2>{},
+                          std::integral_constant<int, KSK - 2>{}, min(s_lo, KS - KSK - 1), 0);
                 } else {
-                    for (int sd = s_lo; sd <= s_hi; sd += KSK) kpass(std::integral_constant<int, KSK>{}, min(sd, KS - KSK), sd);
+                    for (int sd = s_lo; sd <= s_hi; sd += KSK)
+                        kpass(std::integral_constant<int, KSK>{}, std::integral_constant<int, KSK>{}, I{},
+                              min(sd, KS - KSK), sd);
                 }
                 // lane (kh, m) holds C[h][nb][i] = block h's candidate 4 kh + i, view 16 nb + m
                 uint32_t pmv[NH], gdv[NH];
