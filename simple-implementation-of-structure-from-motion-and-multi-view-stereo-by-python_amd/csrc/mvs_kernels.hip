@@ -950,17 +950,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         q += Q[y + NB - 1] - Q[y - 1];
                     }
                     const int db = NPX * q - sg * sg;   // < 2^31: n * sum g^2 <= 121 * 121 * 255^2
-                    // constant window: ctNcc's nan, never passes.  FAST stores 0
-                    // instead (num w_b = 0 < T there too), so that a rejected
-                    // pair's zero term of the avg sum stays zero
-                    double w = FAST ? 0.0 : __builtin_nan("");
-                    if (db > 0) {
-                        // v_rsq_f64 + one Newton step: max relative error 4.1e-15 over
-                        // 4M values of D < 2^31 (tools/ubench/rsq_acc.hip; 5.2e-8 without)
-                        const double D = (double)db;
-                        w = __builtin_amdgcn_rsq(D);
-                        w = w * (1.5 - 0.5 * D * w * w);
-                    }
+                    // v_rsq_f64 + one Newton step: max relative error 4.1e-15 over
+                    // 4M values of D < 2^31 (tools/ubench/rsq_acc.hip; 5.2e-8 without).
+                    // A constant window (D = 0) gets rsq = inf and then nan from the
+                    // Newton step: ctNcc's nan, which never passes (no select)
+                    const double D = (double)db;
+                    double w = __builtin_amdgcn_rsq(D);
+                    w = w * (1.5 - 0.5 * D * w * w);
                     ms[y] = sg - 128 * NPX;             // S_b of s = g - 128
                     mw[y] = w;
                 }
@@ -980,8 +976,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                 for (int k = tid; k < 128 * (VP - V); k += kMmaThreads) {
                     const int px = k / (VP - V), v = V + (k - px * (VP - V));
                     tsb[px * VP + v] = 0;
-                    tw[px * VP + v] = FAST ? 0.0 : __builtin_nan("");
-                    if constexpr (WF) twf[px * VP + v] = FAST ? 0.0f : __builtin_nanf("");
+                    tw[px * VP + v] = __builtin_nan("");
+                    if constexpr (WF) twf[px * VP + v] = __builtin_nanf("");
                 }
             __syncthreads();
             STAMP(t2);
@@ -2197,7 +2193,7 @@ int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipSt
         // the largest table is sized for V = 16 NBLK; every V of this NBLK fits in it
         const int lds = mma_layout<WID, NBLK>(16 * NBLK).total;
         const int used = mma_layout<WID, NBLK>(sc->V).total;
-        if (a->thr >= 0.01) {   // FAST: T > 0 (a constant window's w = 0 can never pass)
+        if (fabs(a->thr) >= 0.01) {
             if (set_dyn_lds_once((const void*)k_score_mma<WID, NBLK, true>, attr_fast, lds) != 0) return -1;
             hipLaunchKernelGGL((k_score_mma<WID, NBLK, true>), dim3(kMmaGrid), dim3(kMmaThreads), used, s, *sc, *a,
                                *t, (const int4*)t->items, (const int2*)t->sorted);
