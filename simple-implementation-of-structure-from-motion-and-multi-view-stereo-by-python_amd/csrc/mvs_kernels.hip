@@ -105,7 +105,10 @@ DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fe
     uint32_t Sb[NS], Sbb[NS], Sab[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) Sb[s] = Sbb[s] = Sab[s] = 0;
-#pragma unroll 1
+    // one view slot: every row's loads in flight at once (a latency-bound
+    // wave per candidate); more slots: one row at a time (registers)
+    constexpr int ROW_UNROLL = NS == 1 ? NB : 1;
+#pragma unroll ROW_UNROLL
     for (int row = 0; row < NB; ++row) {
         uint32_t w[NS][NW];
 #pragma unroll
@@ -337,11 +340,19 @@ template <bool LDSHIST>
 __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t, int wid) {
     extern __shared__ int32_t hist[];      // [ntiles] local counts, then global bases
+    // the cameras' projection constants (R', t, fx fy cx cy) in LDS: every
+    // candidate reads its reference camera's 16 values there instead of by
+    // per-lane global loads
+    __shared__ double s_cam[MVS_MAX_VIEWS][16];
     const int words = (sc.V + 63) >> 6;
-    if (LDSHIST) {
-        for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
-        __syncthreads();
+    for (int k = threadIdx.x; k < sc.V * 16; k += blockDim.x) {
+        const int v = k >> 4, f = k & 15;
+        const CamDev& cm = sc.cams[v];
+        s_cam[v][f] = f < 9 ? cm.Rp[f] : f < 12 ? cm.t[f - 9] : f == 12 ? cm.fx : f == 13 ? cm.fy : f == 14 ? cm.cx : cm.cy;
     }
+    if (LDSHIST)
+        for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
     int tl[kBinPer], lr[kBinPer];
 #pragma unroll
@@ -352,7 +363,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         const int R = a.ref[i];
         const double c[3] = {a.c[3 * i], a.c[3 * i + 1], a.c[3 * i + 2]};
         double px, py;
-        project(sc.cams[R], c, px, py);
+        project_vals(s_cam[R], c, px, py);
         a.xy[2 * i] = px;
         a.xy[2 * i + 1] = py;
         int q, r;
