@@ -53,7 +53,7 @@ PEAK_HBM = 8.0e12          # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
 PEAK_I8 = 5.0e15           # dense i8 MFMA ops/s (2x the 2.5 PF dense bf16; no sparsity)
 SIMDS = 1024               # 256 CUs x 4 SIMDs
 CLOCK = 2.4e9              # peak engine clock, Hz
-PMC_PATH = os.path.join(REPO, "profiles", "r02", "pmc.json")
+PMC_PATH = os.path.join(REPO, "profiles", "r03", "pmc.json")
 # kernel / score-call timing: HIP and torch events on every TIME_EVERY-th timed step
 TIME_EVERY = 5
 
