@@ -131,6 +131,31 @@ def roofline(entry, V, wid, n, kms):
     return out
 
 
+def exchange_figures(ctx, sw, V, vlb, accepted, world, stream):
+    """The per-sweep exchange's payload and its device pack time (HIP events
+    over 20 packs of this rank's scored sweep on the scoring stream), and the
+    all-gather each rank receives at N = 8."""
+    import torch
+    par = importlib.import_module(PKG_NAME + ".parallel")
+    words = (V + 63) // 64
+    row = 8 * par.points_width(words)
+    cap = accepted + accepted // 16 + 256
+    out = torch.empty((cap + 1, par.points_width(words)), dtype=torch.int64, device=sw["count"].device)
+    for _ in range(3):
+        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(20):
+        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream)
+    e1.record(stream)
+    e1.synchronize()
+    return {"row_bytes": row, "rows_per_rank": accepted, "bytes_per_rank": row * (cap + 1),
+            "pack_us": e0.elapsed_time(e1) / 20 * 1e3,
+            "received_per_rank_at_n8_MB": 7 * row * (cap + 1) / 1e6,
+            "note": "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync); the "
+                    "all-gather runs on its own stream behind the next sweep (parallel.PointsExchange)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,7 +244,7 @@ def main():
             if exchange and world > 1:
                 # pack (device, no host sync) + all-gather on the exchange's own
                 # stream, overlapping the next sweep (parallel.PointsExchange)
-                sw["exch"].post(sw["off"], sw["count"], sw["mask"], sw["c"], vlb, stream=stream)
+                sw["exch"].post(sw["off"], sw["count"], sw["mask"], vlb, stream=stream)
 
         for _ in range(warmup):
             step()
@@ -290,7 +315,7 @@ def main():
         "config": {"workload": f"{'dinoRing' if a.scene == 'dino' else 'sphere ring'} {V}x{W}x{H}, "
                                f"one expansion sweep of {n} candidates per GPU, "
                                f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
-                               f"MIN_NCC {a.thr}, accepted records (with 3D points) all-gathered",
+                               f"MIN_NCC {a.thr}, accepted records (index + view mask) all-gathered",
                    "global_batch": total_n, "wid": a.wid, "views": V,
                    "parallelism": f"candidate-queue shards x{world} (RCCL all-gather of accepted points)"},
         "kernel": kernel_name,
@@ -298,6 +323,7 @@ def main():
         "score_call_ms": pms,
         "accepted_per_sweep": accepted,
         "gathered_records": gathered,
+        "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream),
     }
     out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n), V, a.wid, n, kms)
 

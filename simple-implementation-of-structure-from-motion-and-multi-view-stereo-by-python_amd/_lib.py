@@ -33,7 +33,7 @@ SIGNATURES = [
                                  _dp, _u64p, _i32p, _dp]),
     ("mvs_score_device", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int,
                                         ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
-    ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
+    ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, ctypes.c_int,
                                          ctypes.c_int64, _vp, _vp]),
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
                                            _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
@@ -308,17 +308,17 @@ class MvsContext:
                                      stream if stream is not None else None)
         check(rc, self._h, "mvs_score_device")
 
-    def pack_accepted(self, offset, count, mask, c, vlb, out, stream=None):
+    def pack_accepted(self, offset, count, mask, vlb, out, stream=None):
         """mvs_pack_accepted: the accepted candidates (count >= vlb) of a scored
-        slice as exchange rows of out (device int64 tensor (cap + 1, 1 + words + 3):
-        row 0 = [accepted, n, cap, 0...], then [offset + i, mask words, x y z bits]
-        in index order); stream-ordered, no host sync."""
+        slice as exchange rows of out (device int64 tensor (cap + 1, 1 + words):
+        row 0 = [accepted, n, 0...], then [offset + i, mask words] in index
+        order); stream-ordered, no host sync."""
         n = int(count.numel())
         cap = int(out.shape[0]) - 1
-        if out.dtype.itemsize != 8 or out.shape[1] != 1 + self.words + 3 or not out.is_contiguous():
-            raise RuntimeError("pack_accepted: out must be contiguous int64 (cap + 1, 1 + words + 3)")
+        if out.dtype.itemsize != 8 or out.shape[1] != 1 + self.words or not out.is_contiguous():
+            raise RuntimeError("pack_accepted: out must be contiguous int64 (cap + 1, 1 + words)")
         rc = load().mvs_pack_accepted(self._h, n, int(offset), count.data_ptr(), mask.data_ptr(),
-                                      c.data_ptr(), int(vlb), cap, out.data_ptr(),
+                                      int(vlb), cap, out.data_ptr(),
                                       stream if stream is not None else None)
         check(rc, self._h, "mvs_pack_accepted")
 

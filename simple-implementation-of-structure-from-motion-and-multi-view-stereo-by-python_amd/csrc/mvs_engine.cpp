@@ -1390,15 +1390,15 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
 }
 
 int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count, const uint64_t* d_mask,
-                      const double* d_c, int vlb, int64_t cap, int64_t* d_out, void* stream) {
+                      int vlb, int64_t cap, int64_t* d_out, void* stream) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
-    if (n < 0 || cap < 0 || !d_out || (n > 0 && (!d_count || !d_mask || !d_c)))
+    if (n < 0 || cap < 0 || !d_out || (n > 0 && (!d_count || !d_mask)))
         return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
     return guarded(ctx, [&]() {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         ctx->scratch_acquire(s);
         ctx->p_chunk.ensure(std::max<int64_t>((n + 1023) / 1024, 1));
-        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, ctx->words(), d_c, vlb, cap, ctx->p_chunk.p,
+        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, ctx->words(), vlb, cap, ctx->p_chunk.p,
                                      d_out, s) != 0)
             throw Fail{MVS_E_HIP, "pack launch failed"};
         ctx->scratch_release(s);

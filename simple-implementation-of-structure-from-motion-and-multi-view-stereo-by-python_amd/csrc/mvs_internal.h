@@ -163,8 +163,7 @@ int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hip
 // index order, at most cap rows (parallel.PointsExchange); chunk_acc holds
 // ceil(n / 1024) int32
 int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, int words,
-                             const double* c, int vlb, int64_t cap, int32_t* chunk_acc, int64_t* out,
-                             hipStream_t s);
+                             int vlb, int64_t cap, int32_t* chunk_acc, int64_t* out, hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
                            int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
 // stage output order on the device (reconstruct_from_Q, MVS2.py:159-173):

@@ -561,7 +561,7 @@ DEV double fma_f64_lanes(double acc, int num, double w, uint64_t P) {
         "s_mov_b64 exec, %[save]"
         : [acc] "+v"(acc), [t] "=&v"(t), [save] "=&s"(save)
         : [num] "v"(num), [w] "v"(w), [p] "s"(P)
-        : "exec", "scc");
+        : "scc");   // EXEC is restored before the statement ends
     return acc;
 }
 
@@ -670,7 +670,7 @@ __host__ __device__ constexpr MmaLds mma_lds(int V) {
 // static LDS of k_score_mma: region and candidate buffers (DB) + small slots
 template <int WID, int NBLK, bool DB>
 __host__ __device__ constexpr int mma_static_lds() {
-    return (DB ? 2 * (16 * NBLK * MmaGeom<WID>::VS + kMmaChunk * 8) : 64) + 8 + 4 + 65 * 8 + 64 +
+    return (DB ? 2 * (16 * NBLK * MmaGeom<WID>::VS + 16 + kMmaChunk * 8) : 64) + 8 + 4 + 65 * 8 + 64 +
            kSortBins * kMmaWaves * 3;   // the row sort's counts and offsets
 }
 
@@ -724,8 +724,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     // DB: the two region and candidate buffers are distinct LDS objects, so
     // that the compiler sees that reads of one do not alias the LDS-DMA into
     // the other (no vmcnt wait for the prefetch before them)
+    // (DB) each region buffer ends in 16 zero bytes, never an LDS-DMA target:
+    // phase 3 reads a window row or the zeros by an offset select inside the
+    // one buffer, so that the read keeps the buffer's alias scope and does not
+    // wait for the other buffer's LDS-DMA (a select between two LDS objects
+    // would wait for every LDS-DMA in flight)
     constexpr int RB = DB ? VP * VS : 16, CB = DB ? kMmaChunk * 8 : 16;
-    __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB], s_reg1[RB];
+    __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB + 16], s_reg1[RB + 16];
     __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[CB];
     __shared__ int s_ids[2];
     __shared__ int s_simd_n[4];
@@ -754,7 +759,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     float* twf = (float*)(smem + L.wf);
     CandInfo* ci = (CandInfo*)(smem + L.ci) + wave * 32;
     if (tid < 8) ((uint32_t*)(smem + L.zero))[tid] = 0u;
-    const uint8_t* zrow = smem + L.zero;
+    if (DB && tid >= 8 && tid < 16) ((uint32_t*)((tid < 12 ? s_reg0 : s_reg1) + RB))[tid & 3] = 0u;
+    const int zoff = DB ? RB : L.zero - L.reg;   // the zero row, relative to a region buffer
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
@@ -1100,11 +1106,11 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                     constexpr int NST = decltype(nstc)::value;
                     constexpr int SAFE_LO = decltype(safe_lo_c)::value, SAFE_HI = decltype(safe_hi_c)::value;
                     uint32_t rbp[NH];
-                    const uint8_t* aptr[NH];
+                    int aoff[NH];
     #pragma unroll
                     for (int h = 0; h < NH; ++h) {
                         rbp[h] = (rb[h] & ~((1u << (2 * sd)) - 1u)) >> (2 * sb);
-                        aptr[h] = reg + Rv[h] * VS + lofs + 64 * sb;
+                        aoff[h] = Rv[h] * VS + lofs + 64 * sb;
                     }
                     const uint8_t* bptr[NBLK];
     #pragma unroll
@@ -1116,10 +1122,11 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                     auto load = [&](int st, int slot) {
     #pragma unroll
                         for (int h = 0; h < NH; ++h)
-                            // rows outside the window read 16 zero bytes: an address
+                            // rows outside the window read 16 zero bytes: an offset
                             // select instead of a branch around the load
-                            av[slot][h] = *(const uint4*)((st >= SAFE_LO && st <= SAFE_HI) || ((rbp[h] >> (2 * st)) & 1u)
-                                                              ? aptr[h] + 64 * st : zrow);
+                            av[slot][h] = *(const uint4*)(reg + ((st >= SAFE_LO && st <= SAFE_HI) ||
+                                                                         ((rbp[h] >> (2 * st)) & 1u)
+                                                                     ? aoff[h] + 64 * st : zoff));
     #pragma unroll
                         for (int nb = 0; nb < NBLK; ++nb) bv[slot][nb] = *(const uint4*)(bptr[nb] + 64 * st);
                     };
@@ -1317,19 +1324,28 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
 // each).  A workgroup takes one work item (the candidates of one 16x8 tile,
 // at most kGroupChunk of them) from the queue and scores it against every
 // view group in turn:
+//   0. (per item) the candidate list is sorted by the candidate's row in the
+//      tile (counting sort over 8 rows), so that an M-block of 16 candidates
+//      spans few region rows and its K-loop skips the K-steps none of its
+//      windows reaches;
 //   1. (per item) each candidate's own reference window rows go to LDS by
-//      LDS-DMA (its view is usually in another group); its S_a, w_a and
-//      decision constants from them;
-//   2. (per group) D = n S_bb - S_b^2 of every (pixel, view) of the group
-//      (int32; -1 for a constant window): one thread per (pixel column, view)
-//      sums its column's window rows straight from the staged region (masked
-//      v_dot4_i32_i8) and slides them down the tile;
+//      LDS-DMA (its view is usually in another group); behind group 0's
+//      phase 2 they are masked in place to the window's columns (the A
+//      operands need no masking afterwards), S_a and S_aa summed per row by
+//      every thread, and the decision constants derived;
+//   2. (per group) Q = S_bb of every (pixel, view) of the group (int32; -1
+//      past V): one thread per (pixel column, view) sums its column's window
+//      rows straight from the staged region (masked v_dot4_i32_i8) and slides
+//      them down the tile;
 //   3. (per group) wave tasks (M-block of 16 candidates, 32 views): C = sum
 //      s_R s_v and S_b = sum s_v over the window, both by
-//      v_mfma_i32_16x16x64_i8 (S_b with the window's 0/1 indicator as A);
-//      num = n C - S_a S_b; the decision num w_b > T in binary32 with
-//      w_b = v_rsq_f32(D) (guard band 2e-6 |T| as in k_score_mma), the sum
-//      of the passing num w_b with w_b refined in binary64 (one Newton step);
+//      v_mfma_i32_16x16x64_i8 (S_b with the window's 0/1 indicator row as A,
+//      from a 16-entry table by the window's column); D = n Q - S_b^2 and
+//      num = n C - S_a S_b (24-bit multiplies: |S_b| < 2^14, Q < 2^21); the
+//      decision num w_b > T in binary32 with w_b = v_rsq_f32(D) (guard band
+//      2e-6 |T| as in k_score_mma; D = 0, a constant window, gives
+//      0 * inf = nan and never passes), the sum of the passing num w_b with
+//      w_b refined in binary64 (one Newton step);
 //   4. (per group) each candidate's mask word, count, sum and guard flag
 //      accumulate in its thread's registers; written after the last group
 //      (guard-band candidates to k_score_fix).
@@ -1341,25 +1357,26 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
 // write.  Work items come tile-major (k_tile_scan): the workgroups in flight
 // share image rows, so TLB and L2 reach over 256 views of a large image.
 // ---------------------------------------------------------------------------
-constexpr int kVTab = 68;   // D-table row pitch (int32): the per-column writes are conflict free
+constexpr int kVTab = 68;   // Q-table row pitch (int32): the per-column writes are conflict free
 
 // a candidate's constants (LDS, per item)
 struct alignas(16) CandInfoV {
-    int32_t px, R, Sa, pk;    // D-table row of its pixel (px * kVTab), reference view, -S_a, packed pixel
+    int32_t px, R, Sa, pk;    // Q-table row of its pixel (px * kVTab), reference view, -S_a, packed pixel
     float T, gT;              // decision threshold on num w_b and its guard band
     double ca;                // n / (n-1) * w_a
 };
 
 // dynamic LDS of k_score_mma_v (the LDS-DMA targets are static arrays)
 struct VLds {
-    int dtab, ci, rmask, rguard, rsum, total;
+    int qtab, ci, rmask, rguard, rsum, total;
 };
 
 __host__ __device__ constexpr VLds v_lds() {
     VLds L{};
-    L.dtab = 0;                                                 // [128 px][kVTab] int32
-    L.ci = L.dtab + 128 * kVTab * 4;
-    L.rmask = L.ci + kGroupChunk * (int)sizeof(CandInfoV);      // [cand][4 view blocks] u16
+    L.qtab = 0;                                                 // [128 px][kVTab] int32
+    L.ci = L.qtab + 128 * kVTab * 4;
+    L.rmask = L.ci + kGroupChunk * (int)sizeof(CandInfoV);      // [cand][4 view blocks] u16 (item start:
+                                                                // [cand] {S_a, S_aa} int32 sums)
     L.rguard = L.rmask + kGroupChunk * 4 * 2;                   // [cand][2 halves] u16
     L.rsum = L.rguard + kGroupChunk * 2 * 2 + 8;                // [cand][2 halves] double (8-B aligned)
     L.total = L.rsum + kGroupChunk * 2 * 8;
@@ -1368,7 +1385,8 @@ __host__ __device__ constexpr VLds v_lds() {
 
 template <int WID>
 __host__ __device__ constexpr int v_static_lds() {
-    return 2 * 64 * MmaGeom<WID>::VS + 2 * kGroupChunk * 8 + kGroupChunk * MmaGeom<WID>::NB * 32 + 32;
+    return 2 * 64 * MmaGeom<WID>::VS + 2 * kGroupChunk * 8 + kGroupChunk * MmaGeom<WID>::NB * 32 + 16 +
+           16 * 32 + 16 + 16 + 16 * 4;
 }
 
 // Workgroup barrier for LDS traffic: every wave's LDS operations are complete
@@ -1407,18 +1425,27 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                                                              const int4* __restrict__ items,
                                                              const int2* __restrict__ sorted) {
     using G = MmaGeom<WID>;
-    constexpr int NB = G::NB, NPX = G::NPX, ROWS = G::ROWS, KS = G::KS, VS = G::VS, C0 = G::C0;
+    constexpr int NB = G::NB, NPX = G::NPX, ROWS = G::ROWS, VS = G::VS, C0 = G::C0;
     constexpr int RPV = VS / 32;
     constexpr int NPIECE = 64 * RPV * 2;                                              // 16-B pieces of a region
     constexpr int RPIECE = (NPIECE + kMmaThreads - 1) / kMmaThreads;                  // ... per thread
     constexpr int APIECE = (kGroupChunk * NB * 2 + kMmaThreads - 1) / kMmaThreads;   // reference-row pieces
-    static_assert(kGroupChunk <= 128, "one phase-3 task per wave");
-    // LDS-DMA targets: two regions, two candidate lists, the reference rows
+    constexpr int AROW = (kGroupChunk * NB + kMmaThreads - 1) / kMmaThreads;         // reference rows per thread
+    static_assert(kGroupChunk <= 128, "one phase-3 task per wave; the sort ranks two waves");
+    // LDS-DMA targets: two regions, the candidate list as it lands (s_cd0) and
+    // sorted by row (s_cd1), the reference rows
     __shared__ __attribute__((aligned(16))) uint8_t s_rg0[64 * VS], s_rg1[64 * VS];
     __shared__ __attribute__((aligned(16))) uint8_t s_cd0[kGroupChunk * 8], s_cd1[kGroupChunk * 8];
-    __shared__ __attribute__((aligned(16))) uint8_t s_areg[kGroupChunk * NB * 32];
+    // the reference rows, then 16 zero bytes (never an LDS-DMA target): phase
+    // 3 reads a row or the zeros through an offset select inside the one
+    // array, so that the read carries the array's alias scope and waits for
+    // no LDS-DMA in flight (a select between two arrays would wait for all)
+    constexpr int AZERO = kGroupChunk * NB * 32;
+    __shared__ __attribute__((aligned(16))) uint8_t s_areg[AZERO + 16];
+    // the window indicator rows by window column (0/1 bytes), then 16 zeros
+    __shared__ __attribute__((aligned(16))) uint8_t s_ind[16 * 32 + 16];
     __shared__ int s_item;
-    __shared__ uint4 s_zero;
+    __shared__ __attribute__((aligned(16))) int32_t s_cnt[16];   // the sort's per-wave row counts
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr VLds L = v_lds();
     const int tid = threadIdx.x;
@@ -1426,9 +1453,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     const int V = sc.V;
     const int NG = t.groups;
     const int words = (V + 63) >> 6;
-    int32_t* dtab = (int32_t*)(smem + L.dtab);
+    int32_t* qtab = (int32_t*)(smem + L.qtab);
     CandInfoV* ci = (CandInfoV*)(smem + L.ci);
     uint16_t* rmask = (uint16_t*)(smem + L.rmask);
+    int32_t* asums = (int32_t*)(smem + L.rmask);   // item start only: {S_a, S_aa} per candidate
     uint16_t* rguard = (uint16_t*)(smem + L.rguard);
     double* rsum = (double*)(smem + L.rsum);
     const double kn = (double)NPX / (double)(NPX - 1);
@@ -1458,34 +1486,67 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                                                  16, 0, 0);
         }
     };
-    auto stage_cands = [&](const int4 d, auto bufc) {
+    // an item's candidate list always lands in s_cd0 (free once sorted into s_cd1)
+    auto stage_cands = [&](const int4 d) {
         const int32_t* csrc = (const int32_t*)(sorted + d.y);
         if (tid < 2 * d.z)
             __builtin_amdgcn_global_load_lds((const void*)(csrc + tid),
-                                             (void __attribute__((address_space(3)))*)((decltype(bufc)::value ? s_cd1 : s_cd0) + wave * 64 * 4),
+                                             (void __attribute__((address_space(3)))*)(s_cd0 + wave * 64 * 4),
                                              4, 0, 0);
     };
 
-    // the first item: its candidates and group 0's region
-    if (tid == 0) {
-        s_item = atomicAdd(head, 1);
-        s_zero = make_uint4(0u, 0u, 0u, 0u);
+    // the first item: its candidates and group 0's region; the indicator rows
+    if (tid == 0) s_item = atomicAdd(head, 1);
+    if (tid < 16 * 8) {   // indicator row q: bytes [q + C0, q + C0 + NB) are 1
+        const int q = tid >> 3, j = tid & 7;
+        const uint32_t wm = ((1u << NB) - 1u) << (q + C0);
+        ((uint32_t*)s_ind)[tid] = byte_mask((wm >> (4 * j)) & 15u) & 0x01010101u;
+    } else if (tid < 16 * 8 + 4) {
+        ((uint32_t*)(s_ind + 16 * 32))[tid - 16 * 8] = 0u;
+        ((uint32_t*)(s_areg + AZERO))[tid - 16 * 8] = 0u;
     }
     __syncthreads();
     int item = __builtin_amdgcn_readfirstlane(s_item);
     if (item >= n_items) return;
     int4 d = items[item];
-    stage_cands(d, std::integral_constant<int, 0>{});
+    stage_cands(d);
     stage_region(d.x, 0, std::integral_constant<int, 0>{});
     __syncthreads();
-    int par = 0;     // candidate-list buffer of this item
     int kpar = 0;    // region buffer of this group (groups alternate across items)
 
     for (;;) {
         const int tile = d.x, nc = d.z;
         const int ty = tile / t.ntx;
         const int x0 = (tile - ty * t.ntx) * MVS_TILE_W;
-        const int2* cand = (const int2*)(par ? s_cd1 : s_cd0);
+        const int2* cand = (const int2*)s_cd1;
+        // ---- 0. the candidates sorted by row (counting sort, two waves) ----
+        {
+            const int2 e = tid < nc ? ((const int2*)s_cd0)[tid] : make_int2(0, 0);
+            const int key = (e.y >> 4) & 7;
+            int rank = 0;
+            if (wave < 2) {
+                int cntv = 0;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const uint64_t m = __ballot(tid < nc && key == r);
+                    if ((tid & 63) == r) cntv = __popcll(m);
+                    if (key == r) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                }
+                if ((tid & 63) < 8) s_cnt[wave * 8 + (tid & 63)] = cntv;
+            }
+            if (tid < 2 * kGroupChunk) asums[tid] = 0;
+            lds_barrier();
+            if (tid < nc) {
+                int pos = rank;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int c0 = s_cnt[r], c1 = s_cnt[8 + r];
+                    pos += (r < key ? c0 + c1 : 0) + (r == key && wave == 1 ? c0 : 0);
+                }
+                ((int2*)s_cd1)[pos] = e;
+            }
+            lds_barrier();
+        }
         const int my_idx = tid < nc ? cand[tid].x : 0;
         // ---- 1. the candidates' reference rows (they land behind phase 2) ----
         // (the candidate entries are read first: an LDS read between two
@@ -1541,8 +1602,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 if (!last) {
                     stage_region(tile, g + 1, std::integral_constant<int, buf ^ 1>{});
                 } else if (next < n_items) {
-                    if (par) stage_cands(dn, std::integral_constant<int, 0>{});
-                    else stage_cands(dn, std::integral_constant<int, 1>{});
+                    stage_cands(dn);
                     stage_region(dn.x, 0, std::integral_constant<int, buf ^ 1>{});
                 }
             };
@@ -1552,39 +1612,33 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             // read in it would make the compiler drain every load at loop entry)
             int claim = 0;
             if (g == 0 && tid == 0) claim = atomicAdd(head, 1);
-            // ---- 2. D of every (pixel, view) of the group ----
+            // ---- 2. Q = S_bb of every (pixel, view) of the group ----
+#ifdef MVS_DIAG_NOPHASE2
+            if (false) {
+#else
             if (mv < GV) {
+#endif
                 // rows in order, the window sliding down as they come: at most
                 // NB + 1 row sums live
-                int S[ROWS], Q[ROWS];
+                int Q[ROWS];
                 const uint8_t* col = reg + mv * VS + 4 * cd0;
-                int s = 0, q = 0;
+                int q = 0;
 #pragma unroll
                 for (int rho = 0; rho < ROWS; ++rho) {
-                    int sr = 0, qr = 0;
+                    int qr = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int dm = (int)(*(const uint32_t*)(col + rho * 32 + 4 * j) & cmk[j]);
-                        sr = __builtin_amdgcn_sdot4(dm, 0x01010101, sr, false);
                         qr = __builtin_amdgcn_sdot4(dm, dm, qr, false);
                     }
-                    S[rho] = sr;
                     Q[rho] = qr;
-                    s += sr;
                     q += qr;
-                    if (rho >= NB) {
-                        s -= S[rho - NB];
-                        q -= Q[rho - NB];
-                    }
-                    if (rho >= NB - 1) {
-                        const int y = rho - (NB - 1);
-                        const int D = NPX * q - s * s;   // < 2^31: n * sum s^2 <= 121 * 121 * 128^2
-                        dtab[(y * 16 + mx) * kVTab + mv] = D > 0 ? D : -1;   // -1: v_rsq_f32 gives nan, never passes
-                    }
+                    if (rho >= NB) q -= Q[rho - NB];
+                    if (rho >= NB - 1) qtab[((rho - (NB - 1)) * 16 + mx) * kVTab + mv] = q;
                 }
             } else {
 #pragma unroll
-                for (int y = 0; y < MVS_TILE_H; ++y) dtab[(y * 16 + mx) * kVTab + mv] = -1;
+                for (int y = 0; y < MVS_TILE_H; ++y) qtab[(y * 16 + mx) * kVTab + mv] = -1;   // D < 0: nan
             }
             STAMP(t0a);
             // (and, group 0, the reference rows have landed; nothing else is in
@@ -1592,23 +1646,43 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             __syncthreads();
             STAMP(t0b);
             if (g == 0) {
-                if (tid == 0) s_item = claim;   // published by the barrier below
-                // the candidates' constants from their reference rows
+                if (tid == 0) s_item = claim;   // published by the barriers below
+                // the reference rows masked in place to their window's columns,
+                // and their sums: one thread per (candidate, row)
+#pragma unroll
+                for (int p = 0; p < AROW; ++p) {
+                    const int k = tid + p * kMmaThreads;
+                    if (k < nc * NB) {
+                        const int qrel = cand[k / NB].y & 15;
+                        const uint32_t wm = ((1u << NB) - 1u) << (qrel + C0);
+                        uint4* row = (uint4*)(s_areg + k * 32);
+                        uint4 h0 = row[0], h1 = row[1];
+                        h0.x &= byte_mask(wm & 15u);
+                        h0.y &= byte_mask((wm >> 4) & 15u);
+                        h0.z &= byte_mask((wm >> 8) & 15u);
+                        h0.w &= byte_mask((wm >> 12) & 15u);
+                        h1.x &= byte_mask((wm >> 16) & 15u);
+                        h1.y &= byte_mask((wm >> 20) & 15u);
+                        h1.z &= byte_mask((wm >> 24) & 15u);
+                        h1.w &= byte_mask(wm >> 28);
+                        row[0] = h0;
+                        row[1] = h1;
+                        int s = 0, q = 0;
+                        const uint32_t dw[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            s = __builtin_amdgcn_sdot4((int)dw[j], 0x01010101, s, false);
+                            q = __builtin_amdgcn_sdot4((int)dw[j], (int)dw[j], q, false);
+                        }
+                        atomicAdd(&asums[2 * (k / NB)], s);
+                        atomicAdd(&asums[2 * (k / NB) + 1], q);
+                    }
+                }
+                lds_barrier();
+                // the candidates' constants
                 if (tid < nc) {
                     const int pk = cand[tid].y;
-                    const int qrel = pk & 15;
-                    uint32_t amk[4];
-                    window_dword_masks<NB>(qrel + C0, amk);
-                    const int ad0 = (qrel + C0) >> 2;
-                    int s = 0, q = 0;
-#pragma unroll
-                    for (int j = 0; j < NB; ++j)
-#pragma unroll
-                        for (int k4 = 0; k4 < 4; ++k4) {
-                            const int dm = (int)(*(const uint32_t*)(s_areg + (tid * NB + j) * 32 + 4 * (ad0 + k4)) & amk[k4]);
-                            s = __builtin_amdgcn_sdot4(dm, 0x01010101, s, false);
-                            q = __builtin_amdgcn_sdot4(dm, dm, q, false);
-                        }
+                    const int s = asums[2 * tid], q = asums[2 * tid + 1];
                     const double wa = rsqrt_nr(NPX * q - s * s);
                     CandInfoV c;
                     c.px = (pk & 127) * kVTab;
@@ -1630,6 +1704,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             // (the barrier after phase 4 waits for it with the region's LDS-DMA)
             if (g > 0 && tid < nc) a.mask[(int64_t)my_idx * words + g - 1] = pend;
             asm volatile("" ::: "memory");   // the LDS-DMA issues stay ahead of phase 3
+            STAMP(tpf);
 
             // ---- 3. wave task (M-block b, views 32 h + [0, 32)) ----
             const int nblk = (nc + 15) >> 4;
@@ -1639,29 +1714,38 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 const bool valid = kk < nc;
                 const int pk = valid ? ci[kk].pk : 0;
                 const int qrel = pk & 15, rrel = (pk >> 4) & 7;
-                const uint32_t wm = valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u;
-                const uint32_t hm = wm >> (16 * (kh & 1));
-                uint32_t cm[4], cmi[4];
-#pragma unroll
-                for (int k4 = 0; k4 < 4; ++k4) {
-                    cm[k4] = byte_mask((hm >> (4 * k4)) & 15u);
-                    cmi[k4] = cm[k4] & 0x01010101u;
-                }
+                // the block's rows (sorted): K-steps s0..s1 hold every window row
+                const int r_lo = __builtin_amdgcn_readfirstlane((ci[b * 16].pk >> 4) & 7);
+                const int r_hi = __builtin_amdgcn_readfirstlane((ci[min(b * 16 + 15, nc - 1)].pk >> 4) & 7);
+                const int s0 = r_lo >> 1, s1 = (r_hi + NB - 1) >> 1;
                 const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
                 // region row 2s + (kh >> 1) = window row 2s + (kh >> 1) - rrel of the candidate
-                const uint8_t* aptr = s_areg + (min(kk, nc - 1) * NB - rrel) * 32 + 16 * (kh & 1);
+                const int aoff = (min(kk, nc - 1) * NB - rrel) * 32 + 16 * (kh & 1);
+                const int ioff = qrel * 32 + 16 * (kh & 1);
+#ifdef MVS_DIAG_AISEL
+                uint32_t cmi[4];
+                {
+                    const uint32_t hm = (valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u) >> (16 * (kh & 1));
+#pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) cmi[k4] = byte_mask((hm >> (4 * k4)) & 15u) & 0x01010101u;
+                }
+#endif
                 const uint8_t* bptr0 = reg + min(32 * h + m, GV - 1) * VS + lofs;
                 const uint8_t* bptr1 = reg + min(32 * h + 16 + m, GV - 1) * VS + lofs;
                 v4i C0v = {0, 0, 0, 0}, C1v = {0, 0, 0, 0}, S0v = {0, 0, 0, 0}, S1v = {0, 0, 0, 0};
-#pragma unroll
-                for (int s = 0; s < KS; ++s) {
+                auto kstep = [&](const int s) {
                     const int row = 2 * s + (kh >> 1);
                     const bool rv = valid && row >= rrel && row < rrel + NB;
-                    // rows outside the window read 16 zero bytes: an address select
+                    // rows outside the window read 16 zero bytes: an offset select
                     // instead of a branch around the load
-                    const uint4 av = *(const uint4*)(rv ? aptr + row * 32 : (const uint8_t*)&s_zero);
-                    const v4i A = {(int)(av.x & cm[0]), (int)(av.y & cm[1]), (int)(av.z & cm[2]), (int)(av.w & cm[3])};
+                    const uint4 av = *(const uint4*)(s_areg + (rv ? aoff + row * 32 : AZERO));
+#ifdef MVS_DIAG_AISEL
                     const v4i AI = rv ? (v4i){(int)cmi[0], (int)cmi[1], (int)cmi[2], (int)cmi[3]} : (v4i){0, 0, 0, 0};
+#else
+                    const uint4 iv = *(const uint4*)(s_ind + (rv ? ioff : 16 * 32));
+                    const v4i AI = {(int)iv.x, (int)iv.y, (int)iv.z, (int)iv.w};
+#endif
+                    const v4i A = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
                     const uint4 b0 = *(const uint4*)(bptr0 + 64 * s);
                     const uint4 b1 = *(const uint4*)(bptr1 + 64 * s);
                     const v4i B0 = {(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w};
@@ -1670,7 +1754,14 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                     C1v = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B1, C1v, 0, 0, 0);
                     S0v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B0, S0v, 0, 0, 0);
                     S1v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B1, S1v, 0, 0, 0);
-                }
+                };
+                // every window takes KMIN K-steps: those unrolled from sb (loads
+                // issued ahead of the MFMAs), the block's further ones after
+                constexpr int KMIN = (NB + 2) / 2;
+                const int sb = min(s0, G::KS - KMIN);
+#pragma unroll
+                for (int u = 0; u < KMIN; ++u) kstep(sb + u);
+                for (int s = sb + KMIN; s <= s1; ++s) kstep(s);
                 // lane (kh, m) holds candidate 16 b + 4 kh + i, views vb + 32 h + 16 j + m
                 uint32_t pmv = 0, gdv = 0;
                 double sacc[4];
@@ -1682,30 +1773,32 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                     static_for<2>([&](auto Jc) {
                         constexpr int j = Jc;
                         const int vl = 32 * h + 16 * j + m;
-                        const int D = dtab[c.px + vl];
-                        const float wf = __builtin_amdgcn_rsqf((float)D);   // nan for D = -1
-                        const int num = __mul24(c.Sa, j ? S1v[i] : S0v[i]) + __mul24(NPX, j ? C1v[i] : C0v[i]);
+                        const int Sb = j ? S1v[i] : S0v[i];
+                        const int D = __mul24(NPX, qtab[c.px + vl]) - __mul24(Sb, Sb);   // < 0 past V: nan
+                        const float wf = __builtin_amdgcn_rsqf((float)D);
+                        const int num = __mul24(c.Sa, Sb) + __mul24(NPX, j ? C1v[i] : C0v[i]);
                         const uint64_t liv = __builtin_amdgcn_uicmp((uint32_t)(vb + vl), (uint32_t)c.R, 33);
                         // w_b in binary64: one Newton step from the binary32 estimate
                         double w = (double)wf;
                         w = w * (1.5 - 0.5 * (double)D * w * w);
-                        bool pass;
                         uint64_t P, Gd;
                         if constexpr (FAST) {
                             const float x = fmaf((float)num, wf, -c.T);
                             P = __builtin_amdgcn_fcmpf(x, 0.0f, 2) & liv;
-                            pass = __builtin_amdgcn_inverse_ballot_w64(P);   // no second compare
                             Gd = __builtin_amdgcn_fcmpf(fabsf(x), c.gT, 4) & liv;
                         } else {
                             const double ncc = (double)num * w * c.ca;
-                            pass = vb + vl != c.R && ncc > a.thr;
-                            P = __ballot(pass);
+                            P = __ballot(vb + vl != c.R && ncc > a.thr);
                             Gd = __ballot(vb + vl != c.R && fabs(ncc - a.thr) <= kGuard);
                         }
                         pmv = writelane<2 * (2 * i + j)>(pmv, (uint32_t)P);
                         pmv = writelane<2 * (2 * i + j) + 1>(pmv, (uint32_t)(P >> 32));
                         gacc |= Gd;
-                        sa = fma((double)num, pass ? w : 0.0, sa);
+#ifdef MVS_DIAG_SASEL
+                        sa = fma((double)num, __builtin_amdgcn_inverse_ballot_w64(P) ? w : 0.0, sa);
+#else
+                        sa = fma_f64_lanes(sa, num, w, P);
+#endif
                     });
                     gdv = writelane<2 * i>(gdv, (uint32_t)gacc);
                     gdv = writelane<2 * i + 1>(gdv, (uint32_t)(gacc >> 32));
@@ -1758,6 +1851,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             STAMP_ADD(5, t0b - t0a);   // barrier after phase 2 (group 0: the reference rows)
             STAMP_ADD(6, t1 - t0b);    // group 0: the candidate constants
             STAMP_ADD(7, t1a - t1);    // wave 0: prefetch issue + its phase-3 task
+            if (g == 0) STAMP_ADD(8, t0b - t0a);                     // barrier after phase 2, group 0 only
+            STAMP_ADD_LANE0(9, t0a - t0);                            // every wave's own phase-2 work
+            STAMP_ADD(10, tpf - t1);                                 // wave 0: prefetch + mask-store issue
+            if (wave < ((nc + 15) >> 4) * 2) {
+                STAMP_ADD_LANE0(11, t1a - tpf);                      // a task's phase-3 time (waves with tasks)
+                STAMP_ADD_LANE0(12, 1);                              // tasks
+            }
         };
         for (int g = 0; g < NG; ++g) {
             if (kpar) group(g, std::integral_constant<int, 1>{});
@@ -1773,7 +1873,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
         if (next >= n_items) break;
         item = next;
         d = dn;
-        par ^= 1;
     }
 }
 
@@ -2020,13 +2119,12 @@ __global__ __launch_bounds__(kAccChunk) void k_acc_count(int64_t n, const int32_
 }
 
 __global__ __launch_bounds__(kAccChunk) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
-                                                         const uint64_t* __restrict__ mask, int words,
-                                                         const double* __restrict__ c, int vlb, int64_t cap,
+                                                         const uint64_t* __restrict__ mask, int words, int vlb, int64_t cap,
                                                          const int32_t* __restrict__ chunk_acc, int64_t* __restrict__ out) {
     __shared__ int32_t wt[kAccChunk / 64];
     __shared__ int32_t red[kAccChunk / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int width = 1 + words + 3;
+    const int width = 1 + words;
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     // an empty slice still has chunk 0, which writes the header
     for (int64_t b = blockIdx.x; b < (nchunk > 0 ? nchunk : 1); b += gridDim.x) {
@@ -2052,8 +2150,7 @@ __global__ __launch_bounds__(kAccChunk) void k_acc_pack(int64_t n, int64_t offse
             if (threadIdx.x == 0) {
                 out[0] = base;             // accepted in the whole slice
                 out[1] = n;
-                out[2] = cap;
-                for (int q = 3; q < width; ++q) out[q] = 0;
+                for (int q = 2; q < width; ++q) out[q] = 0;
             }
             base = 0;
         }
@@ -2062,7 +2159,6 @@ __global__ __launch_bounds__(kAccChunk) void k_acc_pack(int64_t n, int64_t offse
             int64_t* o = out + (1 + pos) * width;
             o[0] = offset + i;
             for (int q = 0; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
-            for (int q = 0; q < 3; ++q) o[1 + words + q] = __double_as_longlong(c[3 * i + q]);
         }
         __syncthreads();
     }
@@ -2371,13 +2467,13 @@ extern "C" int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hip
 }
 
 extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask,
-                                        int words, const double* c, int vlb, int64_t cap, int32_t* chunk_acc,
+                                        int words, int vlb, int64_t cap, int32_t* chunk_acc,
                                         int64_t* out, hipStream_t s) {
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, 2048));
     if (n > 0) hipLaunchKernelGGL(k_acc_count, dim3(grid), dim3(kAccChunk), 0, s, n, count, vlb, chunk_acc);
     // n == 0 still writes the header (chunk 0 of an empty slice)
-    hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccChunk), 0, s, n, offset, count, mask, words, c, vlb, cap,
+    hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccChunk), 0, s, n, offset, count, mask, words, vlb, cap,
                        chunk_acc, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -144,14 +144,18 @@ def _points_worker(rank, world, port, n, strong, sweeps, out_dir):
         _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
         if ex is None:
             ex = par.PointsExchange(None, 1, n, torch.device("cpu"))
-        bi = ex.post(off, torch.from_numpy(count), torch.from_numpy(mask.view(np.int64)),
-                     torch.from_numpy(np.ascontiguousarray(c)), 3)
-        idx, m, pts = ex.result(bi)
-        out[f"idx{k}"], out[f"mask{k}"], out[f"pts{k}"] = idx.numpy(), m.numpy(), pts.numpy()
+        bi = ex.post(off, torch.from_numpy(count), torch.from_numpy(mask.view(np.int64)), 3)
+        idx, m = ex.result(bi)
+        # the records carry no geometry: a receiving rank regenerates the 3D
+        # point of any global index from the queue's definition
+        if strong:
+            whole = syn.candidates(n, K, R, t, seed=seed)[0]
+        else:
+            whole = np.concatenate([syn.candidates(n, K, R, t, seed=seed + r)[0] for r in range(world)])
+        out[f"idx{k}"], out[f"mask{k}"], out[f"pts{k}"] = idx.numpy(), m.numpy(), whole[idx.numpy()]
     # capacity overflow is reported, not silently truncated
     small = par.PointsExchange(None, 1, 2, torch.device("cpu"))
-    bi = small.post(0, torch.full((10,), 5, dtype=torch.int32), torch.ones((10, 1), dtype=torch.int64),
-                    torch.zeros((10, 3), dtype=torch.float64), 3)
+    bi = small.post(0, torch.full((10,), 5, dtype=torch.int32), torch.ones((10, 1), dtype=torch.int64), 3)
     try:
         small.result(bi)
         out["overflow_raised"] = np.array(False)
@@ -168,8 +172,9 @@ def test_accepted_points_exchange_gloo(tmp_path, orc, dino, world, n, strong):
     pack layout, double-buffered all-gather): the candidate queue split over
     the ranks -- per-rank blocks (weak) or shard_range slices of one queue
     (strong) -- over three consecutive sweeps, and every rank ends each sweep
-    with the whole sweep's accepted candidates (|V| >= 3), masks and 3D points,
-    in index order, as one process scoring the whole queue finds them."""
+    with the whole sweep's accepted candidates (|V| >= 3) and masks in index
+    order (16-B records), as one process scoring the whole queue finds them,
+    and regenerates their 3D points from the global indices."""
     import importlib
     syn = importlib.import_module(PKG_NAME + ".synthetic")
     sweeps = 3

@@ -52,6 +52,13 @@ labels = ([(1, "D table (+ item constants)"), (4, "  wave 0 own D-table work"), 
           [(1, "staging"), (2, "moments"), (6, "  hsum"), (7, "  vsum"), (3, "candidates")])
 for k, name in labels:
     print(f"  {name:28s} {d[act, k].sum() / tot:9.0f} cycles per {'(item, group)' if scene == 'ring256' else 'item'}")
+if scene == "ring256":
+    g0 = tot / 4.0
+    print(f"  group-0 barrier after phase 2 {d[act, 8].sum() / g0:9.0f} cycles per group 0; other groups "
+          f"{(d[act, 5].sum() - d[act, 8].sum()) / max(tot - g0, 1):9.0f}")
+    print(f"  phase-2 own work, mean of the 16 waves {d[act, 9].sum() / tot / 16:9.0f}; wave 0 prefetch + stores "
+          f"{d[act, 10].sum() / tot:9.0f}")
+    print(f"  phase-3 tasks {d[act, 12].sum() / tot:.2f} per (item, group), {d[act, 11].sum() / max(d[act, 12].sum(), 1):9.0f} cycles each")
 if scene != "ring256":
   print(f"  wave 0: {d[act, 4].sum() / tot:9.0f} cycles of own candidate work per item, "
       f"{d[act, 5].sum() / tot:.2f} M-blocks per item -> {d[act, 4].sum() / max(d[act, 5].sum(), 1):.0f} cycles per M-block")
