@@ -131,7 +131,7 @@ def roofline(entry, V, wid, n, kms):
     return out
 
 
-def exchange_figures(ctx, sw, V, vlb, accepted, world, stream):
+def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
     """The per-sweep exchange's payload and its device pack time (HIP events
     over 20 packs of this rank's scored sweep on the scoring stream), and the
     all-gather each rank receives at N = 8."""
@@ -143,6 +143,12 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream):
     out = torch.empty((cap + 1, par.points_width(words)), dtype=torch.int64, device=sw["count"].device)
     for _ in range(3):
         ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream)
+    # device time: the packs queue up behind three sweeps' worth of scoring,
+    # so the host's submission rate (a ctypes call + two launches per pack,
+    # ~15 us) does not pace them
+    for _ in range(3):
+        ctx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], thr, wid,
+                         stream=stream.cuda_stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(20):
@@ -152,7 +158,8 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream):
     return {"row_bytes": row, "rows_per_rank": accepted, "bytes_per_rank": row * (cap + 1),
             "pack_us": e0.elapsed_time(e1) / 20 * 1e3,
             "received_per_rank_at_n8_MB": 7 * row * (cap + 1) / 1e6,
-            "note": "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync); the "
+            "note": "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync), device time "
+                    "of 20 packs queued behind scoring work; the "
                     "all-gather runs on its own stream behind the next sweep (parallel.PointsExchange)"}
 
 
@@ -323,7 +330,7 @@ def main():
         "score_call_ms": pms,
         "accepted_per_sweep": accepted,
         "gathered_records": gathered,
-        "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream),
+        "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream, a.thr, a.wid),
     }
     out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n), V, a.wid, n, kms)
 

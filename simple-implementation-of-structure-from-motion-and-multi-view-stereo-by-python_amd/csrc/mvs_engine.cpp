@@ -307,7 +307,7 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand;
-    // mvs_pack_accepted: accepted count per 1024-candidate chunk
+    // mvs_pack_accepted: accepted count per 4096-candidate chunk
     DevBuf<int32_t> p_chunk;
     DevBuf<int4> t_items;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
@@ -446,23 +446,30 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.nty = (ctx->H + MVS_TILE_H - 1) / MVS_TILE_H;
         const int ntiles = t.ntx * t.nty;
         const int32_t* tiles_before = ctx->t_tiles.p;
-        ctx->t_tiles.ensure((size_t)3 * (ntiles + 2) + 8);
+        ctx->t_tiles.ensure((size_t)2 * (ntiles + 4) + 8);
         if (ctx->t_tiles.p != tiles_before) ctx->tiles_clean_ntiles = -1;
         const int groups = grouped ? (ctx->V + MVS_GROUP_VIEWS - 1) / MVS_GROUP_VIEWS : 1;
-        ctx->t_cand.ensure((size_t)6 * n);
+        // tile buckets of cap candidates (4x the mean load, at least 1024;
+        // the rest of a tile goes to the direct path), and the direct path's
+        // list (int4 entries)
+        const int64_t mean = (n + ntiles - 1) / ntiles;
+        int64_t cap = std::min<int64_t>(std::max<int64_t>(4 * mean, 1024), std::max<int64_t>(n, 64));
+        cap = (cap + 63) & ~(int64_t)63;
+        if ((int64_t)ntiles * cap >= ((int64_t)1 << 31)) cap = (((int64_t)1 << 31) - 1) / ntiles & ~(int64_t)63;
+        if (cap < 64) throw Fail{MVS_E_UNSUPPORTED, "image too large for the tile buckets"};
+        ctx->t_cand.ensure((size_t)2 * ntiles * cap + 4 * (size_t)n);
         t.ntiles = ntiles;
+        t.cap = (int)cap;
         t.chunk = grouped ? MVS_GROUP_CHUNK : MVS_MMA_CHUNK;
         t.groups = groups;
         t.tile_major = grouped ? 1 : 0;   // k_score_mma_v: neighbouring tiles in flight together
         t.tile_count = ctx->t_tiles.p;
-        t.tile_off = ctx->t_tiles.p + (ntiles + 2);
-        t.item_off = ctx->t_tiles.p + 2 * (ntiles + 2);
         t.fix_count = ctx->t_tiles.p + ntiles + 1;
-        t.cand_key = ctx->t_cand.p;
-        t.cand_rank = ctx->t_cand.p + n;
-        t.cand_pk = ctx->t_cand.p + 2 * n;
-        t.sorted = (int2*)(ctx->t_cand.p + 3 * n);
-        t.fix_list = ctx->t_cand.p + 5 * n;
+        t.ovf_count = ctx->t_tiles.p + ntiles + 2;
+        t.bin_done = ctx->t_tiles.p + ntiles + 3;
+        t.item_off = ctx->t_tiles.p + (ntiles + 4);
+        t.sorted = (int2*)ctx->t_cand.p;
+        t.fix_list = (int4*)(ctx->t_cand.p + 2 * (size_t)ntiles * cap);
         // at most one partial chunk per tile beyond the full ones
         ctx->t_items.ensure((size_t)(n / std::max(t.chunk, 1) + ntiles + 2));
         t.items = ctx->t_items.p;
@@ -475,7 +482,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         if (rc != 0) throw Fail{rc == -3 ? MVS_E_UNSUPPORTED : MVS_E_HIP, "tiled score launch failed"};
         ctx->scratch_release(s);
         if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, 1);
-        ctx->tiles_clean_ntiles = ntiles;        // k_tile_scan leaves the counters zero
+        ctx->tiles_clean_ntiles = ntiles;        // the item scan leaves the counters zero
         return;
     }
     hipEvent_t e0, e1;
@@ -1397,7 +1404,7 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
     return guarded(ctx, [&]() {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         ctx->scratch_acquire(s);
-        ctx->p_chunk.ensure(std::max<int64_t>((n + 1023) / 1024, 1));
+        ctx->p_chunk.ensure(std::max<int64_t>((n + 4095) / 4096, 1));
         if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, ctx->words(), vlb, cap, ctx->p_chunk.p,
                                      d_out, s) != 0)
             throw Fail{MVS_E_HIP, "pack launch failed"};

@@ -56,34 +56,36 @@ struct ScoreArgs {
 };
 
 // Scratch of the tiled scorer (device pointers, sized by the host).
-//   tile_count[ntiles+2], tile_off[ntiles+1], item_off[ntiles+1]
-//   cand_key[n]  = tile (or -1 if the window is invalid), cand_rank[n],
-//   cand_pk[n]   = (x - x0) | (y - y0) << 4 | R << 7 (pixel inside the tile),
-//   sorted[n]    = {id, pk} grouped by tile
-//   fix_list[n], fix_count[1]: candidates with a view decision inside
-//   the guard band, re-scored by k_score_fix (numpy-order ctNcc) afterwards
+//   tile_count[ntiles+4] (counts, queue head, fix_count, ovf_count, bin_done), item_off[ntiles+1]
+//   sorted[ntiles*cap] = {id, pk} per tile bucket (k_bin writes candidate
+//   rank r of tile k at k*cap + r), pk = (x - x0) | (y - y0) << 4 | R << 7
+//   (pixel inside the tile); a candidate of rank >= cap overflows to fix_list
+//   fix_list[n], fix_count: {id, tile, pk, 0} of the candidates k_score_fix
+//   scores by the direct path -- bucket overflow (k_bin, counted in
+//   ovf_count) and candidates with a view decision inside the guard band
+//   (the tiled scorers, numpy-order ctNcc there)
 struct TiledArgs {
     int ntx, nty, ntiles;
     int tw, th;                // tile size in pixels (x, y): 16 x 8
     int chunk;                 // candidates per work item
+    int cap;                   // bucket capacity per tile (candidates)
     int32_t* tile_count;
-    int32_t* tile_off;
     int32_t* item_off;
-    int32_t* cand_key;
-    int32_t* cand_rank;
-    int32_t* cand_pk;
     int2* sorted;
-    int32_t* fix_list;
+    int4* fix_list;
     int32_t* fix_count;
+    int32_t* ovf_count;
+    int32_t* bin_done;         // k_bin workgroups done (the last one scans)
     // view groups of 64 (V > 64: k_score_mma_v scores each work item against
     // every group in turn); groups = 1 otherwise
     int groups;
-    // k_tile_scan leaves every counter zero for the next batch (it zeroes the
-    // bin counts after reading them and the queue head / fix_count before the
-    // scorer uses them); zero_first = 1 asks the launcher to clear them first
-    // (new scratch, or a previous sequence that did not complete)
+    // k_bin's item scan leaves every counter zero for the next batch (it zeroes
+    // the bin counts, ovf_count and bin_done after reading them, the queue head
+    // before the scorer uses it, and starts fix_count at the overflow count); zero_first
+    // = 1 asks the launcher to clear them first (new scratch, or a previous
+    // sequence that did not complete)
     int zero_first;
-    // work items in the order the scorer takes them (k_tile_scan): every full
+    // work items in the order the scorer takes them (the item scan): every full
     // chunk first, then the partial (last) chunks by decreasing size, so the
     // dynamic queue ends on the shortest items; or, tile_major = 1, in tile
     // order; int4 = (tile, first sorted candidate, candidates, 0)
@@ -138,7 +140,7 @@ int mvs_launch_build_scene(const SceneDev* sc, const uint8_t* d_rgb, uint8_t* d_
 // on s immediately before and after the kernel
 int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_t s,
                      hipEvent_t ev0, hipEvent_t ev1);
-// tiled scorer: k_bin, k_tile_scan, k_scatter, k_score_mma or k_score_mma_v
+// tiled scorer: k_bin (tile buckets, then the work items), k_score_mma or k_score_mma_v
 // (timed by ev0/ev1), k_score_fix
 int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
                            hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);

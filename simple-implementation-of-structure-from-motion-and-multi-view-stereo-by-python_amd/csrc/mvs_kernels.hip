@@ -335,6 +335,7 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
 // counters fit in LDS, else through one global atomic per candidate.
 // ---------------------------------------------------------------------------
 constexpr int kBinBlock = 1024, kBinPer = 4, kBinLdsTiles = 16384;
+DEV void tile_scan_block(const TiledArgs& t);   // k_bin's last workgroup
 
 template <bool LDSHIST>
 __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
-    int tl[kBinPer], lr[kBinPer];
+    int tl[kBinPer], lr[kBinPer], pk[kBinPer];
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
@@ -371,13 +372,12 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             for (int w = 0; w < words; ++w) a.mask[i * words + w] = 0;
             a.count[i] = 0;
             if (a.avg) a.avg[i] = 0.0;
-            t.cand_key[i] = -1;
             continue;
         }
         const int tx = q / MVS_TILE_W, ty = r / MVS_TILE_H;
         const int tile = ty * t.ntx + tx;
         tl[k] = tile;
-        t.cand_pk[i] = (q - tx * MVS_TILE_W) | ((r - ty * MVS_TILE_H) << 4) | (R << 7);
+        pk[k] = (q - tx * MVS_TILE_W) | ((r - ty * MVS_TILE_H) << 4) | (R << 7);
         lr[k] = LDSHIST ? atomicAdd(&hist[tile], 1) : atomicAdd(&t.tile_count[tile], 1);
     }
     if (LDSHIST) {
@@ -388,13 +388,28 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         }
         __syncthreads();
     }
+    // straight into the tile's bucket (no separate scatter pass); past the
+    // bucket's capacity to the direct path's list
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
         if (tl[k] < 0) continue;
-        t.cand_key[i] = tl[k];
-        t.cand_rank[i] = (LDSHIST ? hist[tl[k]] : 0) + lr[k];
+        const int rank = (LDSHIST ? hist[tl[k]] : 0) + lr[k];
+        if (rank < t.cap)
+            t.sorted[(int64_t)tl[k] * t.cap + rank] = make_int2((int32_t)i, pk[k]);
+        else
+            t.fix_list[atomicAdd(t.ovf_count, 1)] = make_int4((int32_t)i, tl[k], pk[k], 0);
     }
+    // the last workgroup to get here builds the work items (every count and
+    // overflow atomic of the others has returned before their ticket)
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(t.bin_done, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    tile_scan_block(t);
+    if (threadIdx.x == 0) *t.bin_done = 0;   // clean for the next batch
 }
 
 // Inclusive scan of N values per thread over a 1024-thread block: wave scans
@@ -431,36 +446,41 @@ DEV void block_scan_1024(int32_t (&v)[N], int32_t* wtot /* LDS, 16 * N */) {
         for (int k = 0; k < N; ++k) v[k] += wtot[(wave - 1) * N + k];
 }
 
-// Exclusive scans of tile counts and work items (one workgroup), and the
-// work-item list, either longest-first: all full chunks (tile-major), then
-// the partial chunks by decreasing candidate count (a dynamic queue handed
-// out in that order ends on its shortest items, which trims the tail where a
-// few workgroups still run while the rest of the chip idles), or tile-major
-// (t.tile_major: neighbouring tiles in flight together).
-__global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
-    __shared__ int32_t wtot[16 * 3];
-    __shared__ int32_t tot[3];
+
+// Exclusive scan of the work items (one workgroup) over the tile buckets
+// (min(count, cap) candidates each), and the work-item list, either
+// longest-first: all full chunks (tile-major), then the partial chunks by
+// decreasing candidate count (a dynamic queue handed out in that order ends
+// on its shortest items, which trims the tail where a few workgroups still
+// run while the rest of the chip idles), or tile-major (t.tile_major:
+// neighbouring tiles in flight together).  Run by the last workgroup of
+// k_bin (1024 threads) once every other workgroup has binned its candidates;
+// the counters are read by agent-scope loads (other XCDs updated them).
+DEV int ld_count(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+DEV void tile_scan_block(const TiledArgs& t) {
+    __shared__ int32_t wtot[16 * 2];
+    __shared__ int32_t tot[2];
     __shared__ int32_t hist[1025];                 // partial-chunk sizes (chunk <= 1024)
     const int tid = threadIdx.x;
     const int per = (t.ntiles + 1023) / 1024;
     const int b = tid * per, e = min(b + per, t.ntiles);
-    int32_t v3[3] = {0, 0, 0};                     // candidates, items, full chunks of my tiles
+    int32_t v2[2] = {0, 0};                        // items, full chunks of my tiles
     for (int k = b; k < e; ++k) {
-        const int c = t.tile_count[k];
-        v3[0] += c;
-        v3[1] += (c + t.chunk - 1) / t.chunk;
-        v3[2] += c / t.chunk;
+        const int c = min(ld_count(&t.tile_count[k]), t.cap);
+        v2[0] += (c + t.chunk - 1) / t.chunk;
+        v2[1] += c / t.chunk;
     }
-    const int32_t own[3] = {v3[0], v3[1], v3[2]};
+    const int32_t own[2] = {v2[0], v2[1]};
     for (int s = tid; s <= 1024; s += 1024) hist[s] = 0;
-    block_scan_1024<3>(v3, wtot);
-    if (tid == 1023) { tot[0] = v3[0]; tot[1] = v3[1]; tot[2] = v3[2]; }
+    block_scan_1024<2>(v2, wtot);
+    if (tid == 1023) { tot[0] = v2[0]; tot[1] = v2[1]; }
     for (int k = b; k < e; ++k) {
-        const int rem = t.tile_count[k] % t.chunk;
+        const int rem = min(ld_count(&t.tile_count[k]), t.cap) % t.chunk;
         if (rem) atomicAdd(&hist[rem], 1);
     }
     __syncthreads();
-    const int32_t n_full = tot[2];
+    const int32_t n_full = tot[1];
     {
         // descending exclusive prefix, hist[s] = partials longer than s, as a
         // scan over the sizes in reverse order (thread i <-> size chunk-1-i)
@@ -472,42 +492,32 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const TiledArgs t) {
         if (tid < nsz) hist[t.chunk - 1 - tid] = r1[0] - mine;
         __syncthreads();
     }
-    int32_t rc = v3[0] - own[0], ri = v3[1] - own[1], rf = v3[2] - own[2];
+    int32_t ri = v2[0] - own[0], rf = v2[1] - own[1];
     for (int k = b; k < e; ++k) {
-        t.tile_off[k] = rc;
         t.item_off[k] = ri;
-        const int c = t.tile_count[k];
-        rc += c;
+        const int c = min(ld_count(&t.tile_count[k]), t.cap);
+        const int first = k * t.cap;               // the tile's bucket
         ri += (c + t.chunk - 1) / t.chunk;
         const int full = c / t.chunk, rem = c - full * t.chunk;
         if (t.tile_major) {
             // the tile's chunks at its own item offset
             for (int j = 0; j < full + (rem ? 1 : 0); ++j)
                 t.items[ri - (c + t.chunk - 1) / t.chunk + j] =
-                    make_int4(k, rc - c + j * t.chunk, j < full ? t.chunk : rem, 0);
+                    make_int4(k, first + j * t.chunk, j < full ? t.chunk : rem, 0);
         } else {
-            for (int j = 0; j < full; ++j) t.items[rf + j] = make_int4(k, rc - c + j * t.chunk, t.chunk, 0);
-            if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int4(k, rc - c + full * t.chunk, rem, 0);
+            for (int j = 0; j < full; ++j) t.items[rf + j] = make_int4(k, first + j * t.chunk, t.chunk, 0);
+            if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int4(k, first + full * t.chunk, rem, 0);
         }
         rf += full;
         t.tile_count[k] = 0;          // clean for the next batch's k_bin
     }
-    if (tid == 1023) {
-        t.tile_off[t.ntiles] = tot[0];
-        t.item_off[t.ntiles] = tot[1];
-    }
-    // work-queue head and the fix-list length start this batch at zero
+    if (tid == 1023) t.item_off[t.ntiles] = tot[0];
+    // the work-queue head starts this batch at zero, the direct path's list
+    // after k_bin's overflow entries (whose counter is left clean for the next batch)
     if (tid == 0) {
         t.tile_count[t.ntiles] = 0;
-        t.tile_count[t.ntiles + 1] = 0;
-    }
-}
-
-__global__ void k_scatter(const ScoreArgs a, const TiledArgs t) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int tile = t.cand_key[i];
-        if (tile >= 0) t.sorted[t.tile_off[tile] + t.cand_rank[i]] = make_int2((int32_t)i, t.cand_pk[i]);
+        *t.fix_count = ld_count(t.ovf_count);
+        *t.ovf_count = 0;
     }
 }
 
@@ -523,7 +533,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kMmaThreads = 1024, kMmaWaves = kMmaThreads / 64;
 constexpr int kGroupViews = MVS_GROUP_VIEWS;   // views per view group (V > 64): one mask word
-constexpr int kMmaChunk = MVS_MMA_CHUNK;       // candidates per work item, V <= 64 (k_tile_scan: <= 1024)
+constexpr int kMmaChunk = MVS_MMA_CHUNK;       // candidates per work item, V <= 64 (the item scan: <= 1024)
 constexpr int kGroupChunk = MVS_GROUP_CHUNK;   // candidates per work item, V > 64 (reference windows staged)
 constexpr int kMmaGrid = 256;         // one workgroup per CU; the queue balances
 constexpr int kSortBins = MVS_TILE_H / 2;   // k_score_mma sorts an item's candidates by row pair
@@ -1269,7 +1279,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                             a.avg[idx] = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
                         }
                         if (gg) {
-                            t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)idx;
+                            t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
                             STAMP_ADD_ANY(11, 1);
                         }
                     }
@@ -1354,7 +1364,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
 // next item's candidate list and, behind group 0's phase 2, an item's
 // reference rows.  Every LDS-DMA target is a static LDS array of its own, so
 // that the compiler sees no aliasing with the tables phases 2-4 read and
-// write.  Work items come tile-major (k_tile_scan): the workgroups in flight
+// write.  Work items come tile-major (the item scan): the workgroups in flight
 // share image rows, so TLB and L2 reach over 256 views of a large image.
 // ---------------------------------------------------------------------------
 constexpr int kVTab = 68;   // Q-table row pitch (int32): the per-column writes are conflict free
@@ -1868,7 +1878,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             a.mask[(int64_t)my_idx * words + NG - 1] = pend;
             a.count[my_idx] = acnt;
             if (a.avg) a.avg[my_idx] = acnt ? asum * (1.0 / (double)acnt) : 0.0;
-            if (aguard) t.fix_list[atomicAdd(t.fix_count, 1)] = (int32_t)my_idx;
+            if (aguard) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4(my_idx, tile, cand[tid].y, 0);
         }
         if (next >= n_items) break;
         item = next;
@@ -1885,9 +1895,10 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
     const int words = (sc.V + 63) >> 6;
     for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
          k += gridDim.x * 4) {
-        const int64_t cand = __builtin_amdgcn_readfirstlane(t.fix_list[k]);
-        const int pk = __builtin_amdgcn_readfirstlane(t.cand_pk[cand]);
-        const int tile = __builtin_amdgcn_readfirstlane(t.cand_key[cand]);
+        const int4 f = t.fix_list[k];
+        const int64_t cand = __builtin_amdgcn_readfirstlane(f.x);
+        const int tile = __builtin_amdgcn_readfirstlane(f.y);
+        const int pk = __builtin_amdgcn_readfirstlane(f.z);
         const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
         const int q = tx * MVS_TILE_W + (pk & 15), r = ty * MVS_TILE_H + ((pk >> 4) & 7), R = pk >> 7;
         wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * words, a.count + cand,
@@ -2098,67 +2109,98 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // receiver sees accepted > cap).  Two launches: per-chunk accepted counts,
 // then each chunk's rows at (sum of the earlier chunks' counts) + its rank.
 // ---------------------------------------------------------------------------
-constexpr int kAccChunk = 1024;
+// Chunks of kAccPer x kAccThreads candidates, thread t of a chunk holding
+// candidates chunk + t + kAccThreads j (j < kAccPer): the count reads stay
+// coalesced and a workgroup does enough work to hide its latency.
+constexpr int kAccThreads = 256, kAccPer = 16, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
 
-__global__ __launch_bounds__(kAccChunk) void k_acc_count(int64_t n, const int32_t* __restrict__ count, int vlb,
-                                                          int32_t* __restrict__ chunk_acc) {
-    __shared__ int32_t wt[kAccChunk / 64];
+__global__ __launch_bounds__(kAccThreads) void k_acc_count(int64_t n, const int32_t* __restrict__ count, int vlb,
+                                                           int32_t* __restrict__ chunk_acc) {
+    __shared__ int32_t wt[kAccWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t b = blockIdx.x; b * kAccChunk < n; b += gridDim.x) {
-        const int64_t i = b * kAccChunk + threadIdx.x;
-        const uint64_t m = __ballot(i < n && count[i] >= vlb);
-        if (lane == 0) wt[wave] = __popcll(m);
+        int c[kAccPer];
+#pragma unroll
+        for (int j = 0; j < kAccPer; ++j) {
+            const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+            c[j] = i < n ? count[i] : 0;
+        }
+        int t = 0;
+#pragma unroll
+        for (int j = 0; j < kAccPer; ++j) t += __popcll(__ballot(c[j] >= vlb));
+        if (lane == 0) wt[wave] = t;
         __syncthreads();
         if (threadIdx.x == 0) {
-            int t = 0;
-            for (int w = 0; w < kAccChunk / 64; ++w) t += wt[w];
-            chunk_acc[b] = t;
+            int s = 0;
+#pragma unroll
+            for (int w = 0; w < kAccWaves; ++w) s += wt[w];
+            chunk_acc[b] = s;
         }
         __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(kAccChunk) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
-                                                         const uint64_t* __restrict__ mask, int words, int vlb, int64_t cap,
-                                                         const int32_t* __restrict__ chunk_acc, int64_t* __restrict__ out) {
-    __shared__ int32_t wt[kAccChunk / 64];
-    __shared__ int32_t red[kAccChunk / 64];
+__global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
+                                                          const uint64_t* __restrict__ mask, int words, int vlb, int64_t cap,
+                                                          const int32_t* __restrict__ chunk_acc, int64_t* __restrict__ out) {
+    __shared__ int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
+    __shared__ int64_t s_base;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int width = 1 + words;
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     // an empty slice still has chunk 0, which writes the header
     for (int64_t b = blockIdx.x; b < (nchunk > 0 ? nchunk : 1); b += gridDim.x) {
-        // rows before this chunk: the earlier chunks' counts (chunk 0 also
-        // sums them all for the header)
-        const int64_t lim = b == 0 ? nchunk : b;
-        int64_t part = 0;
-        for (int64_t k = threadIdx.x; k < lim; k += kAccChunk) part += chunk_acc[k];
+        if (wave == 0) {
+            // rows before this chunk: the earlier chunks' counts (chunk 0 sums
+            // them all for the header)
+            const int64_t lim = b == 0 ? nchunk : b;
+            int64_t part = 0;
+            for (int64_t k = lane; k < lim; k += 64) part += chunk_acc[k];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
-        if (lane == 0) red[wave] = (int32_t)part;
-        const int64_t i = b * kAccChunk + threadIdx.x;
-        const bool acc = i < n && count[i] >= vlb;
-        const uint64_t m = __ballot(acc);
-        if (lane == 0) wt[wave] = __popcll(m);
-        __syncthreads();
-        int64_t base = 0, wbase = 0;
-        for (int w = 0; w < kAccChunk / 64; ++w) {
-            base += red[w];
-            wbase += w < wave ? wt[w] : 0;
-        }
-        if (b == 0) {
-            if (threadIdx.x == 0) {
-                out[0] = base;             // accepted in the whole slice
-                out[1] = n;
-                for (int q = 2; q < width; ++q) out[q] = 0;
+            for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+            if (lane == 0) {
+                if (b == 0) {
+                    out[0] = part;             // accepted in the whole slice
+                    out[1] = n;
+                    for (int q = 2; q < width; ++q) out[q] = 0;
+                    part = 0;
+                }
+                s_base = part;
             }
-            base = 0;
         }
-        const int64_t pos = base + wbase + __popcll(m & ((1ull << lane) - 1ull));
-        if (acc && pos < cap) {
-            int64_t* o = out + (1 + pos) * width;
-            o[0] = offset + i;
-            for (int q = 0; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
+        uint64_t m[kAccPer];
+#pragma unroll
+        for (int j = 0; j < kAccPer; ++j) {
+            const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+            m[j] = __ballot(i < n && count[i] >= vlb);
+            if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
+        }
+        __syncthreads();
+        if (wave == 0) {   // exclusive scan of the (j, wave) counts in index order
+            const int x = s_cnt[lane];
+            int incl = x;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += y;
+            }
+            s_cnt[lane] = incl - x;
+        }
+        __syncthreads();
+        const int64_t base = s_base;
+#pragma unroll
+        for (int j = 0; j < kAccPer; ++j) {
+            if ((m[j] >> lane) & 1ull) {
+                const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+                const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
+                                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
+                if (pos < cap) {
+                    int64_t* o = out + (1 + pos) * width;
+                    o[0] = offset + i;
+                    for (int q = 0; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
+                }
+            }
         }
         __syncthreads();
     }
@@ -2323,9 +2365,9 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         sc->V > MVS_MAX_VIEWS)
         return -3;
     // tile counters, the work-queue head (tile_count[ntiles]) and fix_count:
-    // left at zero by the previous batch's k_tile_scan unless zero_first
+    // left at zero by the previous batch's item scan unless zero_first
     if (t->zero_first &&
-        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 2), s) != hipSuccess)
+        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 4), s) != hipSuccess)
         return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);
@@ -2333,9 +2375,6 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         hipLaunchKernelGGL(k_bin<true>, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
     else
         hipLaunchKernelGGL(k_bin<false>, dim3(nbin), dim3(kBinBlock), 0, s, *sc, *a, *t, WID);
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, *t);
-    const int nb = (int)std::min<int64_t>((a->n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, *a, *t);
     int rc = 0;
     {
         TimedLaunch tl(s, ev0, ev1);
@@ -2470,10 +2509,10 @@ extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t
                                         int words, int vlb, int64_t cap, int32_t* chunk_acc,
                                         int64_t* out, hipStream_t s) {
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, 2048));
-    if (n > 0) hipLaunchKernelGGL(k_acc_count, dim3(grid), dim3(kAccChunk), 0, s, n, count, vlb, chunk_acc);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, 4096));
+    if (n > 0) hipLaunchKernelGGL(k_acc_count, dim3(grid), dim3(kAccThreads), 0, s, n, count, vlb, chunk_acc);
     // n == 0 still writes the header (chunk 0 of an empty slice)
-    hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccChunk), 0, s, n, offset, count, mask, words, vlb, cap,
+    hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, words, vlb, cap,
                        chunk_acc, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -105,7 +105,9 @@ def test_score_edge_candidates(kctx, oracle_scene, dino):
 
 
 def test_score_dense_tile(kctx, oracle_scene, dino):
-    """Many candidates in one pixel tile (several LDS work items per tile)."""
+    """Many candidates in one pixel tile: several LDS work items per tile on
+    the tiled path, and the candidates past the tile bucket's capacity (1024
+    here) scored by the direct path from the overflow list."""
     rgb, K, R, t = dino
     rng = np.random.default_rng(9)
     n = 5000
@@ -120,6 +122,7 @@ def test_score_dense_tile(kctx, oracle_scene, dino):
     exp = oracle_scene.score_batch(c, ref, 0.5, 5)
     for g, e in zip(got[:3], exp[:3]):
         assert np.array_equal(g, e)
+    np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
 
 
 def test_score_threshold_on_reference_value(kctx, oracle_scene, dino):

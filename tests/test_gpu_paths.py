@@ -308,6 +308,10 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     s = torch.cuda.current_stream()
     for _ in range(3):
         ctx.pack_accepted(0, count, mask, 3, out, stream=s.cuda_stream)
+    # the packs queue behind scoring work, so that the events time the device
+    # and not the host's submission rate (~15 us per ctypes call + 2 launches)
+    for _ in range(3):
+        ctx.score_device(tc, tr, xy, mask, count, None, 0.7, 5, stream=s.cuda_stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(20):
