@@ -307,8 +307,11 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand;
-    // mvs_pack_accepted: accepted count per 4096-candidate chunk
-    DevBuf<int32_t> p_chunk;
+    // mvs_pack_accepted: the chunks' look-back words (one per 4096
+    // candidates), their epoch and the give-up counter
+    DevBuf<uint64_t> p_status;
+    DevBuf<int32_t> p_err;
+    uint64_t p_epoch = 0;
     DevBuf<int4> t_items;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
     DevBuf<float> f_resp, f_dil;
@@ -449,11 +452,12 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         ctx->t_tiles.ensure((size_t)2 * (ntiles + 4) + 8);
         if (ctx->t_tiles.p != tiles_before) ctx->tiles_clean_ntiles = -1;
         const int groups = grouped ? (ctx->V + MVS_GROUP_VIEWS - 1) / MVS_GROUP_VIEWS : 1;
-        // tile buckets of cap candidates (4x the mean load, at least 1024;
-        // the rest of a tile goes to the direct path), and the direct path's
-        // list (int4 entries)
+        // tile buckets of cap candidates (16x the mean load, at least 1024:
+        // expansion sweeps crowd onto the object's tiles; the rest of a tile
+        // goes to the direct path), and the direct path's list (int4 entries).
+        // Only the filled part of a bucket is ever touched.
         const int64_t mean = (n + ntiles - 1) / ntiles;
-        int64_t cap = std::min<int64_t>(std::max<int64_t>(4 * mean, 1024), std::max<int64_t>(n, 64));
+        int64_t cap = std::min<int64_t>(std::max<int64_t>(16 * mean, 1024), std::max<int64_t>(n, 64));
         cap = (cap + 63) & ~(int64_t)63;
         if ((int64_t)ntiles * cap >= ((int64_t)1 << 31)) cap = (((int64_t)1 << 31) - 1) / ntiles & ~(int64_t)63;
         if (cap < 64) throw Fail{MVS_E_UNSUPPORTED, "image too large for the tile buckets"};
@@ -462,7 +466,14 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.cap = (int)cap;
         t.chunk = grouped ? MVS_GROUP_CHUNK : MVS_MMA_CHUNK;
         t.groups = groups;
-        t.tile_major = grouped ? 1 : 0;   // k_score_mma_v: neighbouring tiles in flight together
+#ifdef MVS_LPT_ITEMS
+        t.tile_major = grouped ? 1 : 0;   // k_score_mma: longest items first (A/B switch)
+#else
+        // items in tile order: neighbouring tiles in flight together, and the
+        // item scan needs no size histogram (its LDS atomics contend on the
+        // few sizes a uniform load has: 2.4k of them cost ~10 us at dinoRing)
+        t.tile_major = 1;
+#endif
         t.tile_count = ctx->t_tiles.p;
         t.fix_count = ctx->t_tiles.p + ntiles + 1;
         t.ovf_count = ctx->t_tiles.p + ntiles + 2;
@@ -1404,9 +1415,19 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
     return guarded(ctx, [&]() {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         ctx->scratch_acquire(s);
-        ctx->p_chunk.ensure(std::max<int64_t>((n + 4095) / 4096, 1));
-        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, ctx->words(), vlb, cap, ctx->p_chunk.p,
-                                     d_out, s) != 0)
+        const uint64_t* st_before = ctx->p_status.p;
+        ctx->p_status.ensure(std::max<int64_t>((n + 4095) / 4096, 1));
+        if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used
+            HIPCHK(hipMemsetAsync(ctx->p_status.p, 0, ctx->p_status.n * sizeof(uint64_t), s));
+            ctx->p_epoch = 0;
+        }
+        if (!ctx->p_err.p) {
+            ctx->p_err.ensure(1);
+            HIPCHK(hipMemsetAsync(ctx->p_err.p, 0, sizeof(int32_t), s));
+        }
+        ctx->p_epoch = ctx->p_epoch % ((1ull << 30) - 1) + 1;   // 1 .. 2^30 - 1
+        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, ctx->words(), vlb, cap, ctx->p_status.p,
+                                     ctx->p_epoch, ctx->p_err.p, d_out, s) != 0)
             throw Fail{MVS_E_HIP, "pack launch failed"};
         ctx->scratch_release(s);
         return 0;

@@ -161,11 +161,14 @@ int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hipStream_t s)
 // of children whose masks another rank scored (geometry already in place)
 int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hipStream_t s);
 // The accepted candidates of a sweep slice as exchange rows [global index,
-// mask words, x y z bits] after a header row [accepted, n, cap, 0...], in
-// index order, at most cap rows (parallel.PointsExchange); chunk_acc holds
-// ceil(n / 1024) int32
+// mask words] after a header row [accepted, n, 0...], in index order, at most
+// cap rows (parallel.PointsExchange), one launch; status holds
+// max(ceil(n / 4096), 1) words of the chunks' look-back, epoch in
+// [1, 2^30) differs from the previous call's on the same status buffer, *err
+// counts look-back waits that gave up (never expected)
 int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, int words,
-                             int vlb, int64_t cap, int32_t* chunk_acc, int64_t* out, hipStream_t s);
+                             int vlb, int64_t cap, uint64_t* status, uint64_t epoch, int32_t* err, int64_t* out,
+                             hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
                            int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
 // stage output order on the device (reconstruct_from_Q, MVS2.py:159-173):

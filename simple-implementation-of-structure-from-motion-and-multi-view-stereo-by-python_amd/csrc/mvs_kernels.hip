@@ -334,8 +334,39 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
 // per block (one global atomic per non-empty (block, tile) pair) when the tile
 // counters fit in LDS, else through one global atomic per candidate.
 // ---------------------------------------------------------------------------
-constexpr int kBinBlock = 1024, kBinPer = 4, kBinLdsTiles = 16384;
-DEV void tile_scan_block(const TiledArgs& t);   // k_bin's last workgroup
+#ifndef MVS_BIN_PER
+#define MVS_BIN_PER 4   // candidates per k_bin thread (A/B switch)
+#endif
+#ifdef MVS_STAMPS
+// diagnostic build only: per-workgroup cycle sums of the scorer's phases
+// (slot 0 items, 1 staging + barrier, 2 moments, 3 candidates, 4 wave 0's own
+// candidate time, 5 wave 0's M-blocks), read by mvs_read_stamps; k_bin's
+// workgroups use rows 2048 + (slot 0 workgroups, 1 projection + LDS ranks,
+// 2 global tile bases, 3 bucket writes + ticket, 4 the item scan)
+__device__ unsigned long long g_stamps[4096 * 16];
+#define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(slot, val) \
+    do { if (threadIdx.x == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
+#define STAMP_ADD_W0(slot, val) \
+    do { if ((threadIdx.x & 1023) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
+// any lane / one lane per wave
+#define STAMP_ADD_ANY(slot, val) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val))
+#define STAMP_ADD_LANE0(slot, val) \
+    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
+#define STAMP_ADD_ROW(row, slot, val) \
+    do { if (threadIdx.x == 0) atomicAdd(&g_stamps[((row) & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
+#else
+#define STAMP_ADD_ROW(row, slot, val)
+#define STAMP(var)
+#define STAMP_ADD(slot, val)
+#define STAMP_ADD_W0(slot, val)
+#define STAMP_ADD_ANY(slot, val)
+#define STAMP_ADD_LANE0(slot, val)
+#endif
+
+constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
+constexpr int kMmaGrid = 256;         // the scorers' workgroups: one per CU; the queue balances
+DEV void tile_scan_block(const TiledArgs& t, int32_t* lcnt);   // k_bin's last workgroup
 
 template <bool LDSHIST>
 __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
@@ -351,6 +382,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         const CamDev& cm = sc.cams[v];
         s_cam[v][f] = f < 9 ? cm.Rp[f] : f < 12 ? cm.t[f - 9] : f == 12 ? cm.fx : f == 13 ? cm.fy : f == 14 ? cm.cx : cm.cy;
     }
+    STAMP(t0);
     if (LDSHIST)
         for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
     __syncthreads();
@@ -380,14 +412,26 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         pk[k] = (q - tx * MVS_TILE_W) | ((r - ty * MVS_TILE_H) << 4) | (R << 7);
         lr[k] = LDSHIST ? atomicAdd(&hist[tile], 1) : atomicAdd(&t.tile_count[tile], 1);
     }
+    STAMP(t1);
     if (LDSHIST) {
+        // the workgroup's base in every tile it touched: every thread's
+        // returning atomics in flight together (ntiles <= 16 x 1024)
         __syncthreads();
-        for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) {
-            const int c = hist[b];
-            hist[b] = c ? atomicAdd(&t.tile_count[b], c) : 0;
+        int bs[kBinLdsTiles / kBinBlock];
+#pragma unroll
+        for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
+            const int b = threadIdx.x + j * kBinBlock;
+            const int c = b < t.ntiles ? hist[b] : 0;
+            bs[j] = c ? atomicAdd(&t.tile_count[b], c) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
+            const int b = threadIdx.x + j * kBinBlock;
+            if (b < t.ntiles) hist[b] = bs[j];
         }
         __syncthreads();
     }
+    STAMP(t2);
     // straight into the tile's bucket (no separate scatter pass); past the
     // bucket's capacity to the direct path's list
 #pragma unroll
@@ -406,10 +450,20 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     __syncthreads();
     if (threadIdx.x == 0) s_last = atomicAdd(t.bin_done, 1) == (int)gridDim.x - 1;
     __syncthreads();
+    STAMP(t3);
+    STAMP_ADD_ROW(2048 + blockIdx.x, 0, 1);
+    STAMP_ADD_ROW(2048 + blockIdx.x, 1, t1 - t0);
+    STAMP_ADD_ROW(2048 + blockIdx.x, 2, t2 - t1);
+    STAMP_ADD_ROW(2048 + blockIdx.x, 3, t3 - t2);
     if (!s_last) return;
-    __threadfence();
-    tile_scan_block(t);
+    // acquire only (the counts are read by agent-scope atomic loads anyway):
+    // __threadfence() would also write this XCD's L2 back, megabytes of the
+    // xy and bucket stores, before the scan could start
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    tile_scan_block(t, LDSHIST ? hist : nullptr);
     if (threadIdx.x == 0) *t.bin_done = 0;   // clean for the next batch
+    STAMP(t4);
+    STAMP_ADD_ROW(2048 + blockIdx.x, 4, t4 - t3);
 }
 
 // Inclusive scan of N values per thread over a 1024-thread block: wave scans
@@ -455,33 +509,52 @@ DEV void block_scan_1024(int32_t (&v)[N], int32_t* wtot /* LDS, 16 * N */) {
 // run while the rest of the chip idles), or tile-major (t.tile_major:
 // neighbouring tiles in flight together).  Run by the last workgroup of
 // k_bin (1024 threads) once every other workgroup has binned its candidates;
-// the counters are read by agent-scope loads (other XCDs updated them).
+// the counters are read by agent-scope loads (other XCDs updated them), all
+// in flight at once into k_bin's LDS histogram (lcnt, ntiles entries) when it
+// has one, else once per pass.
 DEV int ld_count(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-DEV void tile_scan_block(const TiledArgs& t) {
+DEV void tile_scan_block(const TiledArgs& t, int32_t* lcnt) {
     __shared__ int32_t wtot[16 * 2];
     __shared__ int32_t tot[2];
     __shared__ int32_t hist[1025];                 // partial-chunk sizes (chunk <= 1024)
     const int tid = threadIdx.x;
+    if (lcnt) {   // ntiles <= 16 x 1024: every load in flight at once
+        int v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int k = tid + j * 1024;
+            v[j] = k < t.ntiles ? ld_count(&t.tile_count[k]) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int k = tid + j * 1024;
+            if (k < t.ntiles) lcnt[k] = min(v[j], t.cap);
+        }
+        __syncthreads();
+    }
+    auto count = [&](int k) { return lcnt ? lcnt[k] : min(ld_count(&t.tile_count[k]), t.cap); };
     const int per = (t.ntiles + 1023) / 1024;
     const int b = tid * per, e = min(b + per, t.ntiles);
     int32_t v2[2] = {0, 0};                        // items, full chunks of my tiles
     for (int k = b; k < e; ++k) {
-        const int c = min(ld_count(&t.tile_count[k]), t.cap);
+        const int c = count(k);
         v2[0] += (c + t.chunk - 1) / t.chunk;
         v2[1] += c / t.chunk;
     }
     const int32_t own[2] = {v2[0], v2[1]};
-    for (int s = tid; s <= 1024; s += 1024) hist[s] = 0;
+    if (!t.tile_major)
+        for (int s = tid; s <= 1024; s += 1024) hist[s] = 0;
     block_scan_1024<2>(v2, wtot);
     if (tid == 1023) { tot[0] = v2[0]; tot[1] = v2[1]; }
-    for (int k = b; k < e; ++k) {
-        const int rem = min(ld_count(&t.tile_count[k]), t.cap) % t.chunk;
-        if (rem) atomicAdd(&hist[rem], 1);
-    }
+    if (!t.tile_major)
+        for (int k = b; k < e; ++k) {
+            const int rem = count(k) % t.chunk;
+            if (rem) atomicAdd(&hist[rem], 1);
+        }
     __syncthreads();
     const int32_t n_full = tot[1];
-    {
+    if (!t.tile_major) {
         // descending exclusive prefix, hist[s] = partials longer than s, as a
         // scan over the sizes in reverse order (thread i <-> size chunk-1-i)
         const int nsz = t.chunk - 1;
@@ -495,7 +568,7 @@ DEV void tile_scan_block(const TiledArgs& t) {
     int32_t ri = v2[0] - own[0], rf = v2[1] - own[1];
     for (int k = b; k < e; ++k) {
         t.item_off[k] = ri;
-        const int c = min(ld_count(&t.tile_count[k]), t.cap);
+        const int c = count(k);
         const int first = k * t.cap;               // the tile's bucket
         ri += (c + t.chunk - 1) / t.chunk;
         const int full = c / t.chunk, rem = c - full * t.chunk;
@@ -535,7 +608,6 @@ constexpr int kMmaThreads = 1024, kMmaWaves = kMmaThreads / 64;
 constexpr int kGroupViews = MVS_GROUP_VIEWS;   // views per view group (V > 64): one mask word
 constexpr int kMmaChunk = MVS_MMA_CHUNK;       // candidates per work item, V <= 64 (the item scan: <= 1024)
 constexpr int kGroupChunk = MVS_GROUP_CHUNK;   // candidates per work item, V > 64 (reference windows staged)
-constexpr int kMmaGrid = 256;         // one workgroup per CU; the queue balances
 constexpr int kSortBins = MVS_TILE_H / 2;   // k_score_mma sorts an item's candidates by row pair
 
 template <int WID>
@@ -614,27 +686,6 @@ __constant__ constexpr RecipTable c_recip{};
 #define MVS_DIAG_STORE_OK(idx) ((idx) == -7)
 #else
 #define MVS_DIAG_STORE_OK(idx) true
-#endif
-#ifdef MVS_STAMPS
-// diagnostic build only: per-workgroup cycle sums of the scorer's phases
-// (slot 0 items, 1 staging + barrier, 2 moments, 3 candidates, 4 wave 0's own
-// candidate time, 5 wave 0's M-blocks), read by mvs_read_stamps
-__device__ unsigned long long g_stamps[4096 * 16];
-#define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
-#define STAMP_ADD(slot, val) \
-    do { if (threadIdx.x == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
-#define STAMP_ADD_W0(slot, val) \
-    do { if ((threadIdx.x & 1023) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
-// any lane / one lane per wave
-#define STAMP_ADD_ANY(slot, val) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val))
-#define STAMP_ADD_LANE0(slot, val) \
-    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[(blockIdx.x & 4095) * 16 + (slot)], (unsigned long long)(val)); } while (0)
-#else
-#define STAMP(var)
-#define STAMP_ADD(slot, val)
-#define STAMP_ADD_W0(slot, val)
-#define STAMP_ADD_ANY(slot, val)
-#define STAMP_ADD_LANE0(slot, val)
 #endif
 
 // a candidate's constants in phase 3 (per wave, 32 slots: the two M-blocks
@@ -2106,77 +2157,59 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // fixed-capacity buffer whose row 0 is the header [accepted, n, cap, 0, ...].
 // No host synchronisation: the accepted total travels in the header, and a
 // slice with more than cap accepted candidates keeps its first cap rows (the
-// receiver sees accepted > cap).  Two launches: per-chunk accepted counts,
-// then each chunk's rows at (sum of the earlier chunks' counts) + its rank.
+// receiver sees accepted > cap).  Each chunk's rows go to (sum of the earlier
+// chunks' counts) + their rank.
 // ---------------------------------------------------------------------------
 // Chunks of kAccPer x kAccThreads candidates, thread t of a chunk holding
 // candidates chunk + t + kAccThreads j (j < kAccPer): the count reads stay
 // coalesced and a workgroup does enough work to hide its latency.
 constexpr int kAccThreads = 256, kAccPer = 16, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
 
-__global__ __launch_bounds__(kAccThreads) void k_acc_count(int64_t n, const int32_t* __restrict__ count, int vlb,
-                                                           int32_t* __restrict__ chunk_acc) {
-    __shared__ int32_t wt[kAccWaves];
+// One launch: each chunk's rows start after every earlier chunk's accepted
+// count, found by a decoupled look-back over per-chunk status words
+// (epoch << 34 | flag << 32 | value; flag 1 = the chunk's own count, 2 = the
+// inclusive count through it; a word of another epoch is not yet published).
+// Workgroups are dispatched in index order and all of them fit on the chip at
+// once (<= 1024 of 256 threads), so a chunk waits only for earlier chunks'
+// workgroups, which are running; a spin limit still bounds every wait (on
+// expiry the chunk counts from 0 and *err is raised).  The words are relaxed
+// agent-scope atomics: a word carries all a reader needs, and a release or
+// acquire would write back or invalidate this XCD's L2 at every step.
+constexpr int kAccGrid = 1024;
+constexpr uint32_t kAccSpin = 1u << 22;
+
+__global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
+                                                          const uint64_t* __restrict__ mask, int words, int vlb, int64_t cap,
+                                                          uint64_t* __restrict__ status, uint64_t epoch,
+                                                          int32_t* __restrict__ err, int64_t* __restrict__ out) {
+    __shared__ int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
+    __shared__ int64_t s_base;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t b = blockIdx.x; b * kAccChunk < n; b += gridDim.x) {
+    const int width = 1 + words;
+    const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
+    const uint64_t E = epoch << 34;
+    // an empty slice still has chunk 0, which writes the header
+    for (int64_t b = blockIdx.x; b < (nchunk > 0 ? nchunk : 1); b += gridDim.x) {
+        // every load of the chunk in flight at once: the counts, then the
+        // accepted candidates' first mask words
         int c[kAccPer];
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
             c[j] = i < n ? count[i] : 0;
         }
-        int t = 0;
-#pragma unroll
-        for (int j = 0; j < kAccPer; ++j) t += __popcll(__ballot(c[j] >= vlb));
-        if (lane == 0) wt[wave] = t;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int s = 0;
-#pragma unroll
-            for (int w = 0; w < kAccWaves; ++w) s += wt[w];
-            chunk_acc[b] = s;
-        }
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
-                                                          const uint64_t* __restrict__ mask, int words, int vlb, int64_t cap,
-                                                          const int32_t* __restrict__ chunk_acc, int64_t* __restrict__ out) {
-    __shared__ int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
-    __shared__ int64_t s_base;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int width = 1 + words;
-    const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
-    // an empty slice still has chunk 0, which writes the header
-    for (int64_t b = blockIdx.x; b < (nchunk > 0 ? nchunk : 1); b += gridDim.x) {
-        if (wave == 0) {
-            // rows before this chunk: the earlier chunks' counts (chunk 0 sums
-            // them all for the header)
-            const int64_t lim = b == 0 ? nchunk : b;
-            int64_t part = 0;
-            for (int64_t k = lane; k < lim; k += 64) part += chunk_acc[k];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
-            if (lane == 0) {
-                if (b == 0) {
-                    out[0] = part;             // accepted in the whole slice
-                    out[1] = n;
-                    for (int q = 2; q < width; ++q) out[q] = 0;
-                    part = 0;
-                }
-                s_base = part;
-            }
-        }
-        uint64_t m[kAccPer];
+        uint64_t m[kAccPer], w0[kAccPer];
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            m[j] = __ballot(i < n && count[i] >= vlb);
+            const bool acc = i < n && c[j] >= vlb;
+            m[j] = __ballot(acc);
+            w0[j] = acc ? mask[i * words] : 0ull;
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
         }
         __syncthreads();
-        if (wave == 0) {   // exclusive scan of the (j, wave) counts in index order
+        if (wave == 0) {
+            // exclusive scan of the (j, wave) counts in index order
             const int x = s_cnt[lane];
             int incl = x;
 #pragma unroll
@@ -2185,6 +2218,50 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 if (lane >= off) incl += y;
             }
             s_cnt[lane] = incl - x;
+            const uint64_t T = (uint32_t)__shfl(incl, 63, 64);   // this chunk's accepted
+            // publish, then look back over the 64 chunks before b at a time
+            if (lane == 0)
+                __hip_atomic_store(&status[b], E | ((b == 0 ? 2ull : 1ull) << 32) | T, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t excl = 0;
+            int64_t top = b - 1;          // the window's highest chunk
+            uint32_t spins = 0;
+            while (top >= 0) {
+                const int64_t k = top - lane;
+                uint64_t v = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : (E | (2ull << 32));
+                const bool pub = (v & ~((1ull << 34) - 1)) == E;
+                const uint32_t flag = pub ? (uint32_t)(v >> 32) & 3u : 0u;
+                // the nearest inclusive word, and whether every chunk up to it has published
+                const uint64_t incl_m = __ballot(flag == 2), unpub = __ballot(!pub);
+                const int first_incl = incl_m ? __builtin_ctzll(incl_m) : 64;
+                const int first_unpub = unpub ? __builtin_ctzll(unpub) : 64;
+                if (first_unpub < first_incl && first_unpub < 64) {
+                    if (++spins > kAccSpin) {   // never expected: give up, count from 0
+                        if (lane == 0) atomicAdd(err, 1);
+                        break;
+                    }
+                    continue;                   // a chunk in the window has not published yet
+                }
+                // lanes 0..min(first_incl, 63) hold published words to sum
+                uint64_t val = (lane <= first_incl && k >= 0) ? (v & 0xffffffffull) : 0ull;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
+                excl += val;
+                if (first_incl < 64) break;     // reached an inclusive prefix
+                top -= 64;
+            }
+            if (lane == 0) {
+                if (b > 0)
+                    __hip_atomic_store(&status[b], E | (2ull << 32) | (excl + T), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (b == (nchunk > 0 ? nchunk - 1 : 0)) {
+                    out[0] = (int64_t)(excl + T);   // accepted in the whole slice
+                    out[1] = n;
+                    for (int q = 2; q < width; ++q) out[q] = 0;
+                }
+                s_base = (int64_t)excl;
+            }
         }
         __syncthreads();
         const int64_t base = s_base;
@@ -2198,7 +2275,8 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 if (pos < cap) {
                     int64_t* o = out + (1 + pos) * width;
                     o[0] = offset + i;
-                    for (int q = 0; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
+                    o[1] = (int64_t)w0[j];
+                    for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
                 }
             }
         }
@@ -2506,14 +2584,13 @@ extern "C" int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hip
 }
 
 extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask,
-                                        int words, int vlb, int64_t cap, int32_t* chunk_acc,
-                                        int64_t* out, hipStream_t s) {
+                                        int words, int vlb, int64_t cap, uint64_t* status, uint64_t epoch,
+                                        int32_t* err, int64_t* out, hipStream_t s) {
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, 4096));
-    if (n > 0) hipLaunchKernelGGL(k_acc_count, dim3(grid), dim3(kAccThreads), 0, s, n, count, vlb, chunk_acc);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, kAccGrid));
     // n == 0 still writes the header (chunk 0 of an empty slice)
     hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, words, vlb, cap,
-                       chunk_acc, out);
+                       status, epoch, err, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

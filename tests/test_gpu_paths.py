@@ -294,7 +294,9 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     assert acc > 1000
     for cap, off in ((acc + 300, 5 << 20), (acc // 3, 0)):
         out = torch.full((cap + 1, 2), -9, dtype=torch.int64, device=dev)
-        ctx.pack_accepted(off, count, mask, 3, out)
+        torch.cuda.synchronize()
+        ctx.pack_accepted(off, count, mask, 3, out)   # the library's stream
+        torch.cuda.synchronize()
         exp = torch.full((cap + 1, 2), -9, dtype=torch.int64)
         par.pack_accepted_reference(off, count.cpu(), mask.cpu(), 3, exp)
         got = out.cpu()
@@ -302,7 +304,9 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
         assert got[0].tolist() == [acc, n]
         assert torch.equal(got[1:1 + k], exp[1:1 + k])
     empty = torch.full((4, 2), -9, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
     ctx.pack_accepted(0, count[:0], mask[:0], 3, empty)
+    torch.cuda.synchronize()
     assert empty[0].cpu().tolist() == [0, 0]
     out = torch.empty((acc + 300 + 1, 2), dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream()
@@ -321,3 +325,32 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     us = e0.elapsed_time(e1) / 20 * 1e3
     print(f"pack_accepted: {us:.1f} us per 2^20 sweep ({acc} accepted rows)")
     assert us <= 10.0
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4097, 5_000_001])
+def test_pack_accepted_lookback_sizes(pkg, ctx, n):
+    """The pack's one-launch look-back over 4096-candidate chunks: a single
+    partial chunk, a chunk boundary, and more chunks (1,221) than workgroups
+    (1,024), so workgroups take a second chunk whose predecessors belong to
+    other workgroups; synthetic counts/masks against the torch reference,
+    twice in a row (the status words' epoch changes between calls)."""
+    import importlib
+    import torch
+    par = importlib.import_module(pkg.__name__ + ".parallel")
+    g = torch.Generator().manual_seed(n)
+    count = torch.randint(0, 8, (n,), generator=g, dtype=torch.int32)
+    mask = torch.randint(-2**62, 2**62, (n, 1), generator=g, dtype=torch.int64)
+    acc = int((count >= 3).sum())
+    exp = torch.full((acc + 2, 2), -9, dtype=torch.int64)
+    par.pack_accepted_reference(7, count, mask, 3, exp)
+    dc, dm = count.cuda(), mask.cuda()
+    for _ in range(2):
+        out = torch.full((acc + 2, 2), -9, dtype=torch.int64, device="cuda")
+        # the library's own stream (torch's default stream is handle 0, which
+        # the C-ABI reads as "no stream"): synchronise the device around it
+        torch.cuda.synchronize()
+        ctx.pack_accepted(7, dc, dm, 3, out)
+        torch.cuda.synchronize()
+        got = out.cpu()
+        assert got[0].tolist() == [acc, n]
+        assert torch.equal(got[1:1 + acc], exp[1:1 + acc])

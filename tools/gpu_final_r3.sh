@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-3 closing run: GPU tests, smoke(), rocprof kernel stats + PMC passes
+# (tools/gpu_prof_r3.sh, refreshes gpurun_out/pmc.json), then the default
+# bench line with its CPU baselines.  TAG names the outputs.
+export TMPDIR=/tmp
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+T=${TAG:-r3z}
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/${T}_pytest.log; [ $rc -ne 0 ] && { grep -B5 -A40 "FAILED\|Error" gpurun_out/${T}_pytest.log | head -80; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { tail -20 gpurun_out/${T}_smoke.log; exit 1; }
+tail -2 gpurun_out/${T}_smoke.log
+bash tools/gpu_prof_r3.sh $T || exit $?
+timeout -k 10 600 python -u bench.py > gpurun_out/${T}_bench_full.log 2>&1 || { tail -5 gpurun_out/${T}_bench_full.log; exit 1; }
+tail -1 gpurun_out/${T}_bench_full.log | cut -c1-300

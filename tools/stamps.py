@@ -40,7 +40,7 @@ lib.mvs_read_stamps(buf.ctypes.data)
 before = buf.copy()
 ctx.score(c, ref, 0.7, wid)
 lib.mvs_read_stamps(buf.ctypes.data)
-d = (buf - before).reshape(4096, 16).astype(np.float64)
+d = (buf - before).reshape(4096, 16)[:2048].astype(np.float64)   # rows 2048+: k_bin
 items = d[:, 0]
 act = items > 0
 tot = items.sum()
@@ -67,5 +67,11 @@ if scene != "ring256" and d[act, 13].sum() > 0:
           f"slowest wave {d[act, 9].sum() / tot:9.0f}, mean of the 16 waves {d[act, 10].sum() / tot / 16:9.0f}")
     print(f"  units {d[act, 13].sum() / tot:.2f} per item, {d[act, 12].sum() / max(d[act, 13].sum(), 1) * 100:.1f} % span > KSK; "
           f"fix-list appends {d[act, 11].sum() / tot:.2f} per item")
+kb = (buf - before).reshape(4096, 16)[2048:].astype(np.float64)
+kact = kb[:, 0] > 0
+if kact.any():
+    print(f"  k_bin: {kact.sum()} workgroups; per workgroup: projection + LDS ranks {kb[kact, 1].mean():.0f}, "
+          f"global tile bases {kb[kact, 2].mean():.0f}, bucket writes + ticket {kb[kact, 3].mean():.0f} cycles; "
+          f"item scan (last workgroup) {kb[kact, 4].sum():.0f} cycles")
 per_wg = d[act, 1] + d[act, 2] + d[act, 3]
 print(f"  per workgroup {per_wg.mean():.0f} cycles (max {per_wg.max():.0f})")
