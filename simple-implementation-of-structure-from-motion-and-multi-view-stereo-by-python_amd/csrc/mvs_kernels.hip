@@ -519,6 +519,8 @@ DEV void tile_scan_block(const TiledArgs& t, int32_t* lcnt) {
     __shared__ int32_t tot[2];
     __shared__ int32_t hist[1025];                 // partial-chunk sizes (chunk <= 1024)
     const int tid = threadIdx.x;
+    // the overflow count, loaded beside the tile counts (one latency, not two)
+    const int n_ovf = tid == 0 ? ld_count(t.ovf_count) : 0;
     if (lcnt) {   // ntiles <= 16 x 1024: every load in flight at once
         int v[16];
 #pragma unroll
@@ -589,7 +591,7 @@ DEV void tile_scan_block(const TiledArgs& t, int32_t* lcnt) {
     // after k_bin's overflow entries (whose counter is left clean for the next batch)
     if (tid == 0) {
         t.tile_count[t.ntiles] = 0;
-        *t.fix_count = ld_count(t.ovf_count);
+        *t.fix_count = n_ovf;
         *t.ovf_count = 0;
     }
 }
