@@ -9,15 +9,16 @@ one block of a global candidate queue: rank r scores block r (seed r) of a
 queue of N x 2^20 candidates (weak scaling), or with --strong its
 shard_range slice of one 2^20 queue.  A step = score the sweep on the GPU
 (inputs resident in HBM) + the sweep's exchange (N > 1): the accepted
-candidates (|V| >= 3) as rows [index, mask, 3D point] packed on the device
-and all-gathered over RCCL on a second stream, overlapping the next sweep
-(parallel.PointsExchange).
+candidates (|V| >= 3) as 16-B rows [global index, mask word] packed on the
+device (one launch, no host sync) and all-gathered over RCCL on a second
+stream, overlapping the next sweep (parallel.PointsExchange); a candidate's
+3D point is a function of its global index, so receivers regenerate it.
 
 Beside the headline (rank 0 at N = 1 only, so that the driver's N > 1 runs
 stay short):
   roofline     the binding roof of the dominant kernel (k_score_mma) from the
                live kernel time and the per-launch counters of the committed
-               rocprofv3 PMC profile (profiles/r02/pmc.json): HBM bytes,
+               rocprofv3 PMC profile (profiles/r03/pmc.json): HBM bytes,
                VALU-busy cycles, MFMA i8 operations; frac <= 1 each
   cold_sweep   scene setup from the resident images (k_build_scene) + the sweep
   secondary    wid 3 (BASELINE config 2's 7x7 window)

@@ -1,4 +1,4 @@
-"""Merge rocprofv3 --pmc pass directories into profiles/r02/pmc.json: the
+"""Merge rocprofv3 --pmc pass directories into a pmc.json (profiles/r03/): the
 per-launch counters of the scorer kernel (k_score_mma*) for one bench
 configuration.  bench.py reads this file to compute its roofline fractions.
 usage: pmc_json.py OUT.json SCENE V WID N PMC_DIR"""
