@@ -9,10 +9,10 @@ one block of a global candidate queue: rank r scores block r (seed r) of a
 queue of N x 2^20 candidates (weak scaling), or with --strong its
 shard_range slice of one 2^20 queue.  A step = score the sweep on the GPU
 (inputs resident in HBM) + the sweep's exchange (N > 1): the accepted
-candidates (|V| >= 3) as 16-B rows [global index, mask word] packed on the
-device (one launch, no host sync) and all-gathered over RCCL on a second
-stream, overlapping the next sweep (parallel.PointsExchange); a candidate's
-3D point is a function of its global index, so receivers regenerate it.
+candidates (|V| >= 3) as 40-B rows [global index, mask word, x, y, z] -- the
+accepted 3D points themselves -- packed on the device (one launch, no host
+sync) and all-gathered over RCCL on a second stream, overlapping the next
+sweep (parallel.PointsExchange).
 
 Beside the headline (rank 0 at N = 1 only, so that the driver's N > 1 runs
 stay short):
@@ -143,7 +143,7 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
     cap = accepted + accepted // 16 + 256
     out = torch.empty((cap + 1, par.points_width(words)), dtype=torch.int64, device=sw["count"].device)
     for _ in range(3):
-        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream)
+        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream, c=sw["c"])
     # device time: the packs queue up behind three sweeps' worth of scoring,
     # so the host's submission rate (a ctypes call + two launches per pack,
     # ~15 us) does not pace them
@@ -153,13 +153,16 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(20):
-        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream)
+        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream, c=sw["c"])
     e1.record(stream)
     e1.synchronize()
+    if int(out[0, 0].item()) != accepted:
+        raise RuntimeError(f"pack header {int(out[0, 0].item())} != {accepted} accepted")
     return {"row_bytes": row, "rows_per_rank": accepted, "bytes_per_rank": row * (cap + 1),
             "pack_us": e0.elapsed_time(e1) / 20 * 1e3,
             "received_per_rank_at_n8_MB": 7 * row * (cap + 1) / 1e6,
-            "note": "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync), device time "
+            "note": "rows [global index, mask word, x, y, z]: the accepted 3D points themselves; "
+                    "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync), device time "
                     "of 20 packs queued behind scoring work; the "
                     "all-gather runs on its own stream behind the next sweep (parallel.PointsExchange)"}
 
@@ -252,7 +255,7 @@ def main():
             if exchange and world > 1:
                 # pack (device, no host sync) + all-gather on the exchange's own
                 # stream, overlapping the next sweep (parallel.PointsExchange)
-                sw["exch"].post(sw["off"], sw["count"], sw["mask"], vlb, stream=stream)
+                sw["exch"].post(sw["off"], sw["count"], sw["mask"], vlb, stream=stream, c=sw["c"])
 
         for _ in range(warmup):
             step()
@@ -278,7 +281,7 @@ def main():
             raise RuntimeError(f"kernel timing recorded {kl} launches / {kt} ms for {len(timed_steps)} timed steps")
         pms = sum(e0.elapsed_time(e1) for e0, e1 in evs.values()) / len(evs)
         if exchange and world > 1:
-            got["n"] = int(sum(sw["exch"].check()))       # every rank's rows arrived, none over capacity
+            got["n"] = int(sum(sw["exch"].accepted()))    # every rank's rows arrived, none over capacity / failed
         if world > 1:
             tt = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -323,7 +326,7 @@ def main():
         "config": {"workload": f"{'dinoRing' if a.scene == 'dino' else 'sphere ring'} {V}x{W}x{H}, "
                                f"one expansion sweep of {n} candidates per GPU, "
                                f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
-                               f"MIN_NCC {a.thr}, accepted records (index + view mask) all-gathered",
+                               f"MIN_NCC {a.thr}, accepted points (index, view mask, x y z) all-gathered",
                    "global_batch": total_n, "wid": a.wid, "views": V,
                    "parallelism": f"candidate-queue shards x{world} (RCCL all-gather of accepted points)"},
         "kernel": kernel_name,

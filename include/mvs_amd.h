@@ -97,14 +97,21 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
  * reference is single-process).  The accepted candidates
  * (count >= vlb, MVS2.py:256/369) of a slice of n scored candidates are
  * packed, in index order, into d_out[(cap + 1) * width] int64 with
- * width = 1 + words: row 0 = [accepted, n, 0...], row 1 + j =
- * [offset + i, mask words of i] (16 B at V <= 64; every rank regenerates a
- * candidate's geometry from its global index, as the sharded stage does).
+ * width = 1 + words + (d_c ? 3 : 0): row 0 = [accepted, n, 0...], row 1 + j =
+ * [offset + i, mask words of i, and with d_c (the slice's n*3 centres, the
+ * candidates' 3D points) the binary64 bits of x, y, z] (40 B at V <= 64;
+ * d_c = NULL: 16 B, the receiver regenerating a point from its global index).
  * Device pointers, stream-ordered, no host synchronisation (the accepted
  * total is in the header; a slice with more than cap accepted keeps its
- * first cap).  Feeds the all-gather of parallel.PointsExchange. */
+ * first cap).  accepted = -1 in the header means the pack's look-back gave
+ * up (never expected; the rows are then incomplete): the consumer must
+ * raise.  Feeds the all-gather of parallel.PointsExchange. */
 int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count,
-                      const uint64_t* d_mask, int vlb, int64_t cap, int64_t* d_out, void* stream);
+                      const uint64_t* d_mask, const double* d_c, int vlb, int64_t cap, int64_t* d_out,
+                      void* stream);
+/* Tests only: mode > 0 sets the pack's look-back spin limit, mode < 0 makes
+ * chunk -mode (4096 candidates each) give up at once, 0 restores the default. */
+int mvs_pack_debug(mvs_ctx* ctx, int64_t mode);
 /* Kernel timing (measurement only): while enabled, every enable-th scoring
  * call (enable = 1: every call) records a HIP event pair on its stream
  * immediately around the dominant scoring kernel (k_score_mma / k_score_mma_v

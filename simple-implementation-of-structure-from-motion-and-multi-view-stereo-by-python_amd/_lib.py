@@ -33,8 +33,9 @@ SIGNATURES = [
                                  _dp, _u64p, _i32p, _dp]),
     ("mvs_score_device", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int,
                                         ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
-    ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, ctypes.c_int,
+    ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
                                          ctypes.c_int64, _vp, _vp]),
+    ("mvs_pack_debug", ctypes.c_int, [_vp, ctypes.c_int64]),
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
                                            _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
     ("mvs_exact_hits", ctypes.c_int64, [_vp]),
@@ -308,19 +309,30 @@ class MvsContext:
                                      stream if stream is not None else None)
         check(rc, self._h, "mvs_score_device")
 
-    def pack_accepted(self, offset, count, mask, vlb, out, stream=None):
+    def pack_accepted(self, offset, count, mask, vlb, out, stream=None, c=None):
         """mvs_pack_accepted: the accepted candidates (count >= vlb) of a scored
-        slice as exchange rows of out (device int64 tensor (cap + 1, 1 + words):
-        row 0 = [accepted, n, 0...], then [offset + i, mask words] in index
-        order); stream-ordered, no host sync."""
+        slice as exchange rows of out (device int64 tensor (cap + 1, width):
+        row 0 = [accepted, n, 0...] (accepted = -1: the pack failed), then
+        [offset + i, mask words(, x y z bits with c)] in index order); c = the
+        slice's (n, 3) float64 centres or None (width 1 + words [+ 3]);
+        stream-ordered, no host sync."""
         n = int(count.numel())
         cap = int(out.shape[0]) - 1
-        if out.dtype.itemsize != 8 or out.shape[1] != 1 + self.words or not out.is_contiguous():
-            raise RuntimeError("pack_accepted: out must be contiguous int64 (cap + 1, 1 + words)")
+        width = 1 + self.words + (3 if c is not None else 0)
+        if out.dtype.itemsize != 8 or out.shape[1] != width or not out.is_contiguous():
+            raise RuntimeError(f"pack_accepted: out must be contiguous int64 (cap + 1, {width})")
+        if c is not None and (c.dtype.itemsize != 8 or tuple(c.shape) != (n, 3) or not c.is_contiguous()):
+            raise RuntimeError("pack_accepted: c must be contiguous float64 (n, 3)")
         rc = load().mvs_pack_accepted(self._h, n, int(offset), count.data_ptr(), mask.data_ptr(),
+                                      c.data_ptr() if c is not None else None,
                                       int(vlb), cap, out.data_ptr(),
                                       stream if stream is not None else None)
         check(rc, self._h, "mvs_pack_accepted")
+
+    def pack_debug(self, mode=0):
+        """Tests only: the pack's look-back spin limit (mode > 0) or a forced
+        give-up of chunk -mode (mode < 0); 0 = default."""
+        check(load().mvs_pack_debug(self._h, int(mode)), self._h, "mvs_pack_debug")
 
     def harris_points(self, view):
         """getHarrisPoints(imgs[view]) (HarrisFeatures.py:135-161) on the GPU:

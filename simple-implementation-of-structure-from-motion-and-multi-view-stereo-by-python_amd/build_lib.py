@@ -13,8 +13,9 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmvs_amd.so")
 STAMPS_LIB = os.path.join(HERE, "libmvs_amd_stamps.so")   # diagnostic build (-DMVS_STAMPS)
 ASAN_LIB = os.path.join(HERE, "libmvs_amd_asan.so")       # host code under ASan + UBSan (tools/asan_cpu.sh)
-SOURCES = ["mvs_kernels.hip", "sfm_kernels.hip", "mvs_engine.cpp"]
-HEADERS = ["mvs_internal.h", "mvs_device.h", os.path.join("..", "..", "include", "mvs_amd.h")]
+SOURCES = ["mvs_kernels.hip", "mvs_score_tab.hip", "sfm_kernels.hip", "mvs_engine.cpp"]
+HEADERS = ["mvs_internal.h", "mvs_device.h", "mvs_mma.h", os.path.join("..", "..", "include", "mvs_amd.h")]
+OBJDIR = os.path.join(HERE, "build")   # per-source objects (git- and gpurun-ignored)
 ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -30,7 +31,7 @@ def build(force=False, verbose=False, stamps=False, asan=False):
     if not stamps and not asan and not force and not needs_build():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
            # no wave-aggregated global atomics: their immediate wait on the
            # return value would also drain the scorer's LDS-DMA prefetch
            "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
@@ -47,10 +48,24 @@ def build(force=False, verbose=False, stamps=False, asan=False):
             cmd += ["-Xarch_host", f]
     # A/B of code-generation options (e.g. "-mllvm -amdgpu-sched-strategy=iterative-ilp")
     cmd += os.environ.get("MVS_EXTRA_FLAGS", "").split()
-    cmd += ["-o", out + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
+    # one object per source, compiled in parallel, then linked
+    tag = "stamps" if stamps else "asan" if asan else "lib"
+    os.makedirs(OBJDIR, exist_ok=True)
+    objs = [os.path.join(OBJDIR, f"{tag}_{f}.o") for f in SOURCES]
+    procs = []
+    for f, o in zip(SOURCES, objs):
+        c = cmd + ["-c", os.path.join(CSRC, f), "-o", o]
+        if verbose:
+            print(" ".join(c), file=sys.stderr)
+        procs.append(subprocess.Popen(c, cwd=CSRC))
+    bad = [f for f, p in zip(SOURCES, procs) if p.wait() != 0]
+    if bad:
+        raise subprocess.CalledProcessError(1, f"hipcc {bad}")
+    link = [c for c in cmd if c not in ("-mllvm", "-amdgpu-atomic-optimizer-strategy=None")] + \
+        ["-shared", "-o", out + ".tmp"] + objs
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd, cwd=CSRC)
+        print(" ".join(link), file=sys.stderr)
+    subprocess.check_call(link, cwd=CSRC)
     check_undefined(out + ".tmp")
     os.replace(out + ".tmp", out)
     return out

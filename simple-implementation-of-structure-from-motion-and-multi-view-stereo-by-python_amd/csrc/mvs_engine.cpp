@@ -312,12 +312,45 @@ struct mvs_ctx {
     DevBuf<uint64_t> p_status;
     DevBuf<int32_t> p_err;
     uint64_t p_epoch = 0;
+    int64_t pack_debug = 0;   // mvs_pack_debug (tests): spin limit / forced give-up
     DevBuf<int4> t_items;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
     DevBuf<float> f_resp, f_dil;
     DevBuf<uint32_t> f_key, f_desc;
     DevBuf<int32_t> f_rows, f_pts, f_mom, f_best;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
+    // the tiled scorer's window moments (V <= 64): per wid, built on first use
+    // (k_moments), rebuilt with the scene; tab_mode 0 = tables when they fit,
+    // 1 = never (the in-kernel moments of k_score_mma; env MVS_SCORE_KERNEL=mma)
+    int tab_mode = 0;
+    DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
+    DevBuf<double> mom_w[MVS_MAX_WID + 1];
+    bool mom_ok[MVS_MAX_WID + 1] = {};
+    MomentsDev moments(int wid) const {
+        MomentsDev m{};
+        m.sb = mom_sb[wid].p;
+        m.w = mom_w[wid].p;
+        m.VP = 16 * ((V + 15) / 16);
+        m.wid = wid;
+        return m;
+    }
+    // the tables of wid, built on stream s if needed; false when they do not
+    // apply (V > 64, disabled, or more than 2^31 elements)
+    bool ensure_moments(int wid, hipStream_t s) {
+        if (V > MVS_GROUP_VIEWS || tab_mode != 0) return false;
+        const int64_t elems = (int64_t)H * W * (16 * ((V + 15) / 16));
+        if (elems >= ((int64_t)1 << 31)) return false;
+        if (!mom_ok[wid]) {
+            mom_sb[wid].alloc((size_t)elems);
+            mom_w[wid].alloc((size_t)elems);
+            HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
+            HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
+            const MomentsDev m = moments(wid);
+            if (mvs_launch_moments(&sc, &m, s) != 0) throw Fail{MVS_E_HIP, "moments launch failed"};
+            mom_ok[wid] = true;
+        }
+        return true;
+    }
     int tiles_clean_ntiles = -1;   // tile counters known zero for this tile count (-1: unknown)
     // kernel timing (mvs_kernel_timing): one event pair per `timing_period`-th
     // scoring launch (an event record between two kernels costs a few us of
@@ -466,19 +499,10 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.cap = (int)cap;
         t.chunk = grouped ? MVS_GROUP_CHUNK : MVS_MMA_CHUNK;
         t.groups = groups;
-#ifdef MVS_LPT_ITEMS
-        t.tile_major = grouped ? 1 : 0;   // k_score_mma: longest items first (A/B switch)
-#else
-        // items in tile order: neighbouring tiles in flight together, and the
-        // item scan needs no size histogram (its LDS atomics contend on the
-        // few sizes a uniform load has: 2.4k of them cost ~10 us at dinoRing)
-        t.tile_major = 1;
-#endif
         t.tile_count = ctx->t_tiles.p;
         t.fix_count = ctx->t_tiles.p + ntiles + 1;
-        t.ovf_count = ctx->t_tiles.p + ntiles + 2;
-        t.bin_done = ctx->t_tiles.p + ntiles + 3;
-        t.item_off = ctx->t_tiles.p + (ntiles + 4);
+        t.n_items = ctx->t_tiles.p + ntiles + 2;
+        t.done = ctx->t_tiles.p + ntiles + 3;
         t.sorted = (int2*)ctx->t_cand.p;
         t.fix_list = (int4*)(ctx->t_cand.p + 2 * (size_t)ntiles * cap);
         // at most one partial chunk per tile beyond the full ones
@@ -489,11 +513,13 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         hipEvent_t e0, e1;
         ctx->next_events(&e0, &e1);
         ctx->scratch_acquire(s);
-        const int rc = mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, s, e0, e1);
+        const bool tab = ctx->ensure_moments(wid, s);
+        const MomentsDev mt = ctx->moments(wid);
+        const int rc = mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, tab ? &mt : nullptr, s, e0, e1);
         if (rc != 0) throw Fail{rc == -3 ? MVS_E_UNSUPPORTED : MVS_E_HIP, "tiled score launch failed"};
         ctx->scratch_release(s);
-        if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, 1);
-        ctx->tiles_clean_ntiles = ntiles;        // the item scan leaves the counters zero
+        if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, tab ? 2 : 1);
+        ctx->tiles_clean_ntiles = ntiles;        // k_score_fix leaves the counters zero
         return;
     }
     hipEvent_t e0, e1;
@@ -1313,6 +1339,7 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
         if (const char* km = std::getenv("MVS_SCORE_KERNEL")) {
             if (!std::strcmp(km, "direct")) ctx->kernel_mode = 1;
             else if (!std::strcmp(km, "tiled")) ctx->kernel_mode = 2;
+            else if (!std::strcmp(km, "mma")) ctx->tab_mode = 1;   // tiled, in-kernel moments
         }
         return 0;
     });
@@ -1373,6 +1400,12 @@ int mvs_ctx_rebuild(mvs_ctx* ctx, void* stream) {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         if (mvs_launch_build_scene(&ctx->sc, ctx->d_rgb.p, ctx->d_stack.p, ctx->d_gv.p, s) != 0)
             throw Fail{MVS_E_HIP, "build_scene launch failed"};
+        // the window-moment tables built so far follow the scene
+        for (int w = 1; w <= MVS_MAX_WID; ++w)
+            if (ctx->mom_ok[w]) {
+                const MomentsDev m = ctx->moments(w);
+                if (mvs_launch_moments(&ctx->sc, &m, s) != 0) throw Fail{MVS_E_HIP, "moments launch failed"};
+            }
         return 0;
     });
 }
@@ -1408,7 +1441,7 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
 }
 
 int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count, const uint64_t* d_mask,
-                      int vlb, int64_t cap, int64_t* d_out, void* stream) {
+                      const double* d_c, int vlb, int64_t cap, int64_t* d_out, void* stream) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
     if (n < 0 || cap < 0 || !d_out || (n > 0 && (!d_count || !d_mask)))
         return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
@@ -1416,8 +1449,10 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         ctx->scratch_acquire(s);
         const uint64_t* st_before = ctx->p_status.p;
-        ctx->p_status.ensure(std::max<int64_t>((n + 4095) / 4096, 1));
-        if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used
+        // the chunks' words, then the two words of the finishing ticket
+        const int64_t nst = std::max<int64_t>((n + 4095) / 4096, 1);
+        ctx->p_status.ensure(nst + 2);
+        if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used; ticket 0
             HIPCHK(hipMemsetAsync(ctx->p_status.p, 0, ctx->p_status.n * sizeof(uint64_t), s));
             ctx->p_epoch = 0;
         }
@@ -1426,12 +1461,21 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
             HIPCHK(hipMemsetAsync(ctx->p_err.p, 0, sizeof(int32_t), s));
         }
         ctx->p_epoch = ctx->p_epoch % ((1ull << 30) - 1) + 1;   // 1 .. 2^30 - 1
-        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, ctx->words(), vlb, cap, ctx->p_status.p,
-                                     ctx->p_epoch, ctx->p_err.p, d_out, s) != 0)
+        // the ticket words sit after every chunk word the buffer holds (its
+        // size only grows), so a later, larger slice never reads them as status
+        uint64_t* aux = ctx->p_status.p + ctx->p_status.n - 2;
+        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, d_c, ctx->words(), vlb, cap, ctx->p_status.p, aux,
+                                     ctx->p_epoch, ctx->p_err.p, ctx->pack_debug, d_out, s) != 0)
             throw Fail{MVS_E_HIP, "pack launch failed"};
         ctx->scratch_release(s);
         return 0;
     });
+}
+
+int mvs_pack_debug(mvs_ctx* ctx, int64_t mode) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    ctx->pack_debug = mode;
+    return 0;
 }
 
 int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int wid, double min_ncc,

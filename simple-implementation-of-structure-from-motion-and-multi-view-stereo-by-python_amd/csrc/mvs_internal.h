@@ -56,41 +56,50 @@ struct ScoreArgs {
 };
 
 // Scratch of the tiled scorer (device pointers, sized by the host).
-//   tile_count[ntiles+4] (counts, queue head, fix_count, ovf_count, bin_done), item_off[ntiles+1]
+//   tile_count[ntiles+4]: per-tile counts, then the queue head, fix_count,
+//   n_items, done (k_score_fix's finishing ticket)
 //   sorted[ntiles*cap] = {id, pk} per tile bucket (k_bin writes candidate
 //   rank r of tile k at k*cap + r), pk = (x - x0) | (y - y0) << 4 | R << 7
 //   (pixel inside the tile); a candidate of rank >= cap overflows to fix_list
+//   items[n_items] = (tile, chunk j, 0, 0): bucket entries [j chunk, (j+1)
+//   chunk) of the tile, appended by k_bin in the order the chunks were opened
 //   fix_list[n], fix_count: {id, tile, pk, 0} of the candidates k_score_fix
-//   scores by the direct path -- bucket overflow (k_bin, counted in
-//   ovf_count) and candidates with a view decision inside the guard band
-//   (the tiled scorers, numpy-order ctNcc there)
+//   scores by the direct path -- bucket overflow (k_bin) and candidates with
+//   a view decision inside the guard band (the tiled scorers, numpy-order
+//   ctNcc there)
 struct TiledArgs {
     int ntx, nty, ntiles;
     int tw, th;                // tile size in pixels (x, y): 16 x 8
     int chunk;                 // candidates per work item
     int cap;                   // bucket capacity per tile (candidates)
     int32_t* tile_count;
-    int32_t* item_off;
     int2* sorted;
     int4* fix_list;
     int32_t* fix_count;
-    int32_t* ovf_count;
-    int32_t* bin_done;         // k_bin workgroups done (the last one scans)
+    int32_t* n_items;
+    int32_t* done;
     // view groups of 64 (V > 64: k_score_mma_v scores each work item against
     // every group in turn); groups = 1 otherwise
     int groups;
-    // k_bin's item scan leaves every counter zero for the next batch (it zeroes
-    // the bin counts, ovf_count and bin_done after reading them, the queue head
-    // before the scorer uses it, and starts fix_count at the overflow count); zero_first
-    // = 1 asks the launcher to clear them first (new scratch, or a previous
+    // k_score_fix leaves every counter zero for the next batch; zero_first = 1
+    // asks the launcher to clear them first (new scratch, or a previous
     // sequence that did not complete)
     int zero_first;
-    // work items in the order the scorer takes them (the item scan): every full
-    // chunk first, then the partial (last) chunks by decreasing size, so the
-    // dynamic queue ends on the shortest items; or, tile_major = 1, in tile
-    // order; int4 = (tile, first sorted candidate, candidates, 0)
     int4* items;
-    int tile_major;
+};
+
+// Per-scene window moments of the tiled scorer (V <= 64), one table pair per
+// window half-width, built once from the gray stack (k_moments) and read by
+// k_score_tab: for pixel (y, x) with a valid window and view v, element
+// (y * W + x) * VP + v holds S_b = the sum of the signed bytes s = g - 128
+// over the (2 wid + 1)^2 window (int16: |S_b| <= 121 * 128) and
+// w = 1 / sqrt(n S_bb - S_b^2) (v_rsq_f64 + one Newton step; nan for a
+// constant window and for the pad views V <= v < VP).  VP = 16 ceil(V / 16).
+struct MomentsDev {
+    int16_t* sb;
+    double* w;
+    int VP;
+    int wid;
 };
 
 // One expansion child: (parent record, view v of the parent's V list, i in {-1,+1}).
@@ -143,7 +152,12 @@ int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_
 // tiled scorer: k_bin (tile buckets, then the work items), k_score_mma or k_score_mma_v
 // (timed by ev0/ev1), k_score_fix
 int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
-                           hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+                           const MomentsDev* mt, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+// the window-moment tables of one wid (mvs_score_tab.hip)
+int mvs_launch_moments(const SceneDev* sc, const MomentsDev* mt, hipStream_t s);
+// k_score_tab (V <= 64, the moments from the tables); k_bin has run
+int mvs_launch_score_tab(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt,
+                         hipStream_t s);
 // dynamic LDS bytes of k_score_mma (0 if the configuration is unsupported)
 size_t mvs_mma_lds_bytes(int V, int wid);
 // name of the kernel mvs_launch_score / mvs_launch_score_tiled time for (V, wid)
@@ -161,14 +175,16 @@ int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hipStream_t s)
 // of children whose masks another rank scored (geometry already in place)
 int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hipStream_t s);
 // The accepted candidates of a sweep slice as exchange rows [global index,
-// mask words] after a header row [accepted, n, 0...], in index order, at most
-// cap rows (parallel.PointsExchange), one launch; status holds
-// max(ceil(n / 4096), 1) words of the chunks' look-back, epoch in
-// [1, 2^30) differs from the previous call's on the same status buffer, *err
-// counts look-back waits that gave up (never expected)
-int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, int words,
-                             int vlb, int64_t cap, uint64_t* status, uint64_t epoch, int32_t* err, int64_t* out,
-                             hipStream_t s);
+// mask words, (c != null) x y z bits] after a header row [accepted, n, 0...],
+// in index order, at most cap rows (parallel.PointsExchange), one launch;
+// status holds max(ceil(n / 4096), 1) words of the chunks' look-back, aux two
+// words (zero before the first launch: the finishing ticket, the total), epoch
+// in [1, 2^30) differs from the previous call's on the same status buffer,
+// *err counts look-back give-ups (reset by each launch's last chunk, which
+// then writes accepted = -1); debug: see k_acc_pack (0 in production)
+int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, const double* c,
+                             int words, int vlb, int64_t cap, uint64_t* status, uint64_t* aux, uint64_t epoch,
+                             int32_t* err, int64_t debug, int64_t* out, hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
                            int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
 // stage output order on the device (reconstruct_from_Q, MVS2.py:159-173):

@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "mvs_device.h"
+#include "mvs_mma.h"
 
 namespace {
 
@@ -39,34 +40,6 @@ __device__ __noinline__ double exact_ncc_stack(const SceneDev sc, int R, int v, 
         return base[(int64_t)row * sc.row_bytes + (int64_t)(col >> 2) * vstride + view * 4 + (col & 3)];
     };
     return exact_ncc_generic([&](int i) { return px(R, i); }, [&](int i) { return px(v, i); }, NB * NB);
-}
-
-// Binary64 DPP move (both halves), bound_ctrl: every source lane exists.
-template <int CTRL>
-DEV double dpp_f64(double x) {
-    const unsigned long long u = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, true);
-    return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
-// Reduce-scatter of four values over each row of 16 lanes: lane m of a row
-// (m = lane & 15) returns the row sum of x[m & 3], so lanes m < 4 hold the
-// four sums.  Two partner swaps halve the values a lane carries (keep one
-// index, send the other), then two rotations sum the lanes that share the low
-// two bits: 27 VALU instead of four full row sums (48) and a select.
-DEV double row_sum16_x4(const double (&x)[4], int m) {
-    const bool b0 = m & 1, b1 = (m >> 1) & 1;
-    double k0 = b0 ? x[1] : x[0], s0 = b0 ? x[0] : x[1];
-    double k1 = b0 ? x[3] : x[2], s1 = b0 ? x[2] : x[3];
-    k0 += dpp_f64<0xB1>(s0);    // quad_perm [1,0,3,2]: index b0 (+2)
-    k1 += dpp_f64<0xB1>(s1);
-    double kk = b1 ? k1 : k0;
-    const double ss = b1 ? k0 : k1;
-    kk += dpp_f64<0x4E>(ss);    // quad_perm [2,3,0,1]: index b0 + 2 b1
-    kk += dpp_f64<0x124>(kk);   // row_ror:4
-    kk += dpp_f64<0x128>(kk);   // row_ror:8
-    return kk;
 }
 
 DEV double wave_sum(double x) {
@@ -332,7 +305,12 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
 // window centre.  k_bin projects (binary64, reference order), tests the
 // window and ranks the candidate inside its tile -- through an LDS histogram
 // per block (one global atomic per non-empty (block, tile) pair) when the tile
-// counters fit in LDS, else through one global atomic per candidate.
+// counters fit in LDS, else through one global atomic per candidate -- and
+// writes it into the tile's bucket.  The work items need no scan: a tile's
+// chunk j (candidates [j chunk, (j+1) chunk) of its bucket) is opened by the
+// one workgroup whose returned range of ranks covers rank j chunk, which
+// appends (tile, j) to the item list; the scorers read the tile's final count
+// when they take the item (item_desc).
 // ---------------------------------------------------------------------------
 #ifndef MVS_BIN_PER
 #define MVS_BIN_PER 4   // candidates per k_bin thread (A/B switch)
@@ -342,7 +320,7 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
 // (slot 0 items, 1 staging + barrier, 2 moments, 3 candidates, 4 wave 0's own
 // candidate time, 5 wave 0's M-blocks), read by mvs_read_stamps; k_bin's
 // workgroups use rows 2048 + (slot 0 workgroups, 1 projection + LDS ranks,
-// 2 global tile bases, 3 bucket writes + ticket, 4 the item scan)
+// 2 global tile bases and opened items, 3 bucket writes)
 __device__ unsigned long long g_stamps[4096 * 16];
 #define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, val) \
@@ -366,7 +344,12 @@ __device__ unsigned long long g_stamps[4096 * 16];
 
 constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
 constexpr int kMmaGrid = 256;         // the scorers' workgroups: one per CU; the queue balances
-DEV void tile_scan_block(const TiledArgs& t, int32_t* lcnt);   // k_bin's last workgroup
+
+// items opened by ranks [base, base + c) of a tile: chunk j starts at j chunk
+DEV void open_items(const TiledArgs& t, int tile, int base, int c) {
+    for (int j = (base + t.chunk - 1) / t.chunk; j * t.chunk < base + c && j * t.chunk < t.cap; ++j)
+        t.items[atomicAdd(t.n_items, 1)] = make_int4(tile, j, 0, 0);
+}
 
 template <bool LDSHIST>
 __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
@@ -410,7 +393,12 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         const int tile = ty * t.ntx + tx;
         tl[k] = tile;
         pk[k] = (q - tx * MVS_TILE_W) | ((r - ty * MVS_TILE_H) << 4) | (R << 7);
-        lr[k] = LDSHIST ? atomicAdd(&hist[tile], 1) : atomicAdd(&t.tile_count[tile], 1);
+        if (LDSHIST) {
+            lr[k] = atomicAdd(&hist[tile], 1);
+        } else {
+            lr[k] = atomicAdd(&t.tile_count[tile], 1);
+            open_items(t, tile, lr[k], 1);
+        }
     }
     STAMP(t1);
     if (LDSHIST) {
@@ -427,7 +415,11 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
 #pragma unroll
         for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
             const int b = threadIdx.x + j * kBinBlock;
-            if (b < t.ntiles) hist[b] = bs[j];
+            if (b < t.ntiles) {
+                const int c = hist[b];
+                if (c) open_items(t, b, bs[j], c);
+                hist[b] = bs[j];
+            }
         }
         __syncthreads();
     }
@@ -442,158 +434,13 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         if (rank < t.cap)
             t.sorted[(int64_t)tl[k] * t.cap + rank] = make_int2((int32_t)i, pk[k]);
         else
-            t.fix_list[atomicAdd(t.ovf_count, 1)] = make_int4((int32_t)i, tl[k], pk[k], 0);
+            t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)i, tl[k], pk[k], 0);
     }
-    // the last workgroup to get here builds the work items (every count and
-    // overflow atomic of the others has returned before their ticket)
-    __shared__ int s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(t.bin_done, 1) == (int)gridDim.x - 1;
-    __syncthreads();
     STAMP(t3);
     STAMP_ADD_ROW(2048 + blockIdx.x, 0, 1);
     STAMP_ADD_ROW(2048 + blockIdx.x, 1, t1 - t0);
     STAMP_ADD_ROW(2048 + blockIdx.x, 2, t2 - t1);
     STAMP_ADD_ROW(2048 + blockIdx.x, 3, t3 - t2);
-    if (!s_last) return;
-    // acquire only (the counts are read by agent-scope atomic loads anyway):
-    // __threadfence() would also write this XCD's L2 back, megabytes of the
-    // xy and bucket stores, before the scan could start
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    tile_scan_block(t, LDSHIST ? hist : nullptr);
-    if (threadIdx.x == 0) *t.bin_done = 0;   // clean for the next batch
-    STAMP(t4);
-    STAMP_ADD_ROW(2048 + blockIdx.x, 4, t4 - t3);
-}
-
-// Inclusive scan of N values per thread over a 1024-thread block: wave scans
-// by __shfl_up, the 16 wave totals scanned by one wave, two barriers.
-template <int N>
-DEV void block_scan_1024(int32_t (&v)[N], int32_t* wtot /* LDS, 16 * N */) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int32_t y = __shfl_up(v[k], off, 64);
-            if (lane >= off) v[k] += y;
-        }
-    if (lane == 63)
-#pragma unroll
-        for (int k = 0; k < N; ++k) wtot[wave * N + k] = v[k];
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll
-        for (int k = 0; k < N; ++k) {
-            int32_t x = lane < 16 ? wtot[lane * N + k] : 0;
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) {
-                const int32_t y = __shfl_up(x, off, 64);
-                if (lane >= off) x += y;
-            }
-            if (lane < 16) wtot[lane * N + k] = x;
-        }
-    }
-    __syncthreads();
-    if (wave > 0)
-#pragma unroll
-        for (int k = 0; k < N; ++k) v[k] += wtot[(wave - 1) * N + k];
-}
-
-
-// Exclusive scan of the work items (one workgroup) over the tile buckets
-// (min(count, cap) candidates each), and the work-item list, either
-// longest-first: all full chunks (tile-major), then the partial chunks by
-// decreasing candidate count (a dynamic queue handed out in that order ends
-// on its shortest items, which trims the tail where a few workgroups still
-// run while the rest of the chip idles), or tile-major (t.tile_major:
-// neighbouring tiles in flight together).  Run by the last workgroup of
-// k_bin (1024 threads) once every other workgroup has binned its candidates;
-// the counters are read by agent-scope loads (other XCDs updated them), all
-// in flight at once into k_bin's LDS histogram (lcnt, ntiles entries) when it
-// has one, else once per pass.
-DEV int ld_count(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-DEV void tile_scan_block(const TiledArgs& t, int32_t* lcnt) {
-    __shared__ int32_t wtot[16 * 2];
-    __shared__ int32_t tot[2];
-    __shared__ int32_t hist[1025];                 // partial-chunk sizes (chunk <= 1024)
-    const int tid = threadIdx.x;
-    // the overflow count, loaded beside the tile counts (one latency, not two)
-    const int n_ovf = tid == 0 ? ld_count(t.ovf_count) : 0;
-    if (lcnt) {   // ntiles <= 16 x 1024: every load in flight at once
-        int v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int k = tid + j * 1024;
-            v[j] = k < t.ntiles ? ld_count(&t.tile_count[k]) : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int k = tid + j * 1024;
-            if (k < t.ntiles) lcnt[k] = min(v[j], t.cap);
-        }
-        __syncthreads();
-    }
-    auto count = [&](int k) { return lcnt ? lcnt[k] : min(ld_count(&t.tile_count[k]), t.cap); };
-    const int per = (t.ntiles + 1023) / 1024;
-    const int b = tid * per, e = min(b + per, t.ntiles);
-    int32_t v2[2] = {0, 0};                        // items, full chunks of my tiles
-    for (int k = b; k < e; ++k) {
-        const int c = count(k);
-        v2[0] += (c + t.chunk - 1) / t.chunk;
-        v2[1] += c / t.chunk;
-    }
-    const int32_t own[2] = {v2[0], v2[1]};
-    if (!t.tile_major)
-        for (int s = tid; s <= 1024; s += 1024) hist[s] = 0;
-    block_scan_1024<2>(v2, wtot);
-    if (tid == 1023) { tot[0] = v2[0]; tot[1] = v2[1]; }
-    if (!t.tile_major)
-        for (int k = b; k < e; ++k) {
-            const int rem = count(k) % t.chunk;
-            if (rem) atomicAdd(&hist[rem], 1);
-        }
-    __syncthreads();
-    const int32_t n_full = tot[1];
-    if (!t.tile_major) {
-        // descending exclusive prefix, hist[s] = partials longer than s, as a
-        // scan over the sizes in reverse order (thread i <-> size chunk-1-i)
-        const int nsz = t.chunk - 1;
-        const int32_t mine = tid < nsz ? hist[t.chunk - 1 - tid] : 0;
-        int32_t r1[1] = {mine};
-        __syncthreads();                            // everyone has read hist before it is rewritten
-        block_scan_1024<1>(r1, wtot);
-        if (tid < nsz) hist[t.chunk - 1 - tid] = r1[0] - mine;
-        __syncthreads();
-    }
-    int32_t ri = v2[0] - own[0], rf = v2[1] - own[1];
-    for (int k = b; k < e; ++k) {
-        t.item_off[k] = ri;
-        const int c = count(k);
-        const int first = k * t.cap;               // the tile's bucket
-        ri += (c + t.chunk - 1) / t.chunk;
-        const int full = c / t.chunk, rem = c - full * t.chunk;
-        if (t.tile_major) {
-            // the tile's chunks at its own item offset
-            for (int j = 0; j < full + (rem ? 1 : 0); ++j)
-                t.items[ri - (c + t.chunk - 1) / t.chunk + j] =
-                    make_int4(k, first + j * t.chunk, j < full ? t.chunk : rem, 0);
-        } else {
-            for (int j = 0; j < full; ++j) t.items[rf + j] = make_int4(k, first + j * t.chunk, t.chunk, 0);
-            if (rem) t.items[n_full + atomicAdd(&hist[rem], 1)] = make_int4(k, first + full * t.chunk, rem, 0);
-        }
-        rf += full;
-        t.tile_count[k] = 0;          // clean for the next batch's k_bin
-    }
-    if (tid == 1023) t.item_off[t.ntiles] = tot[0];
-    // the work-queue head starts this batch at zero, the direct path's list
-    // after k_bin's overflow entries (whose counter is left clean for the next batch)
-    if (tid == 0) {
-        t.tile_count[t.ntiles] = 0;
-        *t.fix_count = n_ovf;
-        *t.ovf_count = 0;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -604,62 +451,11 @@ DEV void tile_scan_block(const TiledArgs& t, int32_t* lcnt) {
 // (64-view groups).  Both decide each (candidate, view) pair from exact
 // integer window products and moments (see k_score_mma).
 // ---------------------------------------------------------------------------
-typedef int v4i __attribute__((ext_vector_type(4)));
-
 constexpr int kMmaThreads = 1024, kMmaWaves = kMmaThreads / 64;
 constexpr int kGroupViews = MVS_GROUP_VIEWS;   // views per view group (V > 64): one mask word
-constexpr int kMmaChunk = MVS_MMA_CHUNK;       // candidates per work item, V <= 64 (the item scan: <= 1024)
+constexpr int kMmaChunk = MVS_MMA_CHUNK;       // candidates per work item, V <= 64 (<= 1024: the scorers' lists)
 constexpr int kGroupChunk = MVS_GROUP_CHUNK;   // candidates per work item, V > 64 (reference windows staged)
 constexpr int kSortBins = MVS_TILE_H / 2;   // k_score_mma sorts an item's candidates by row pair
-
-template <int WID>
-struct MmaGeom {
-    static constexpr int NB = 2 * WID + 1;
-    static constexpr int NPX = NB * NB;
-    static constexpr int ROWS = MVS_TILE_H + 2 * WID;   // region rows (even)
-    static constexpr int KS = ROWS / 2;                 // K-steps of two region rows
-    static constexpr int VS = ROWS * 32 + 32;           // bytes per view: VS/16 = 2 mod 4, so the
-                                                        // B reads (ds_read_b128) are conflict-free
-    static constexpr int C0 = 8 - WID;                  // region column of the first window column of x0
-    static_assert(C0 >= 0 && C0 + MVS_TILE_W - 1 + NB <= 32, "window must fit the 32 region columns");
-    static_assert(ROWS % 2 == 0, "K-steps take two rows");
-};
-
-// x through an opaque copy: what is computed from it is computed where it is
-// used, not hoisted out of loops into long-lived registers
-DEV int opaque(int x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
-// acc += num * w in the lanes of P only (binary64): EXEC narrowed to P for
-// the conversion and the fma, restored after -- two vector instructions, no
-// select of the term (the compiler's form of the select costs four)
-DEV double fma_f64_lanes(double acc, int num, double w, uint64_t P) {
-    double t;
-    uint64_t save;
-    asm volatile(
-        "s_and_saveexec_b64 %[save], %[p]\n\t"
-        "v_cvt_f64_i32 %[t], %[num]\n\t"
-        "v_fma_f64 %[acc], %[t], %[w], %[acc]\n\t"
-        "s_mov_b64 exec, %[save]"
-        : [acc] "+v"(acc), [t] "=&v"(t), [save] "=&s"(save)
-        : [num] "v"(num), [w] "v"(w), [p] "s"(P)
-        : "scc");   // EXEC is restored before the statement ends
-    return acc;
-}
-
-// 4-bit column mask -> byte mask
-DEV uint32_t byte_mask(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xffu; }
-
-// 1/k for k = 0..64 (entry 0 unused), correctly rounded at compile time
-struct RecipTable {
-    double r[65];
-    constexpr RecipTable() : r() {
-        for (int k = 1; k <= 64; ++k) r[k] = 1.0 / (double)k;
-    }
-};
-__constant__ constexpr RecipTable c_recip{};
 
 // ---------------------------------------------------------------------------
 // k_score_mma (V <= 64).  A workgroup (16 waves) takes one work item (the
@@ -753,26 +549,6 @@ __host__ __device__ constexpr MmaLds mma_layout(int V) {
     return mma_lds<WID, NBLK, mma_wf<WID, NBLK>(), mma_db<WID, NBLK>()>(V);
 }
 
-// v_writelane_b32 (lane LANE of v takes the wave-uniform x) through the LLVM
-// intrinsic, so that the hazard recognizer sees it: a VALU write of the
-// source SGPR (a ballot's v_cmp) needs wait states before v_writelane reads
-// it, which inline asm would hide from the compiler
-extern "C" __device__ int mvs_llvm_writelane(int x, int lane, int v) __asm("llvm.amdgcn.writelane.i32");
-template <int LANE>
-DEV uint32_t writelane(uint32_t v, uint32_t x) {
-    return (uint32_t)mvs_llvm_writelane((int)x, LANE, (int)v);
-}
-
-// f(integral_constant<int, 0>), ..., f(integral_constant<int, N-1>)
-template <class F, int... I>
-DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-DEV void static_for(F&& f) {
-    static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
 template <int WID, int NBLK, bool FAST>
 __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
                                                            const int4* __restrict__ items,
@@ -827,7 +603,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
-    const int n_units = t.item_off[t.ntiles];
+    const int n_units = *t.n_items;
     int32_t* head = &t.tile_count[t.ntiles];
 
     // The region of an item (gv rows, signed bytes) goes to LDS by LDS-DMA
@@ -889,13 +665,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
     int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
     if (cur >= n_units) return;
-    int4 dcur = items[cur];
+    int4 dcur = item_desc(t, items, cur);
     dcur = make_int4(__builtin_amdgcn_readfirstlane(dcur.x), __builtin_amdgcn_readfirstlane(dcur.y),
                      __builtin_amdgcn_readfirstlane(dcur.z), 0);
     stage(dcur, std::integral_constant<int, 0>{});
     // item nx1's descriptor (uniform, scalar loads) and thread 0's claim of
     // the item after it
-    int4 dnx1 = nx1 < n_units ? items[nx1] : make_int4(0, 0, 0, 0);
+    int4 dnx1 = nx1 < n_units ? item_desc(t, items, nx1) : make_int4(0, 0, 0, 0);
     int pend = 0;
     if (tid == 0) pend = atomicAdd(head, 1);
     __syncthreads();   // everyone has read s_ids before they are rewritten
@@ -1070,7 +846,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             }
             int4 dnx2 = make_int4(0, 0, 0, 0);
             if (nx2 < n_units) {
-                dnx2 = items[nx2];
+                dnx2 = item_desc(t, items, nx2);
                 if (tid == 0) pend = atomicAdd(head, 1);
             }
     
@@ -1417,7 +1193,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
 // next item's candidate list and, behind group 0's phase 2, an item's
 // reference rows.  Every LDS-DMA target is a static LDS array of its own, so
 // that the compiler sees no aliasing with the tables phases 2-4 read and
-// write.  Work items come tile-major (the item scan): the workgroups in flight
+// write.  Work items come in the order k_bin opened them (about tile order): the workgroups in flight
 // share image rows, so TLB and L2 reach over 256 views of a large image.
 // ---------------------------------------------------------------------------
 constexpr int kVTab = 68;   // Q-table row pitch (int32): the per-column writes are conflict free
@@ -1451,11 +1227,6 @@ __host__ __device__ constexpr int v_static_lds() {
     return 2 * 64 * MmaGeom<WID>::VS + 2 * kGroupChunk * 8 + kGroupChunk * MmaGeom<WID>::NB * 32 + 16 +
            16 * 32 + 16 + 16 + 16 * 4;
 }
-
-// Workgroup barrier for LDS traffic: every wave's LDS operations are complete
-// first; outstanding global loads and LDS-DMA are not waited for (the fence of
-// __syncthreads would wait for them: vmcnt(0)).
-DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 
 // byte masks of a window of NB bytes starting at byte b0 over the 4 dwords
@@ -1524,7 +1295,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     double* rsum = (double*)(smem + L.rsum);
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
-    const int n_items = t.item_off[t.ntiles];
+    const int n_items = *t.n_items;
     int32_t* head = &t.tile_count[t.ntiles];
 
     // region piece k (view k / 2RPV, row, half) of view group g at a tile: its
@@ -1571,7 +1342,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     __syncthreads();
     int item = __builtin_amdgcn_readfirstlane(s_item);
     if (item >= n_items) return;
-    int4 d = items[item];
+    int4 d = item_desc(t, items, item);
     stage_cands(d);
     stage_region(d.x, 0, std::integral_constant<int, 0>{});
     __syncthreads();
@@ -1759,7 +1530,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 }
                 lds_barrier();
                 next = __builtin_amdgcn_readfirstlane(s_item);
-                if (next < n_items) dn = items[next];
+                if (next < n_items) dn = item_desc(t, items, next);
             }
             STAMP(t1);
             prefetch();
@@ -1940,12 +1711,16 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
 }
 
 // Guard-band candidates of the tiled scorer, re-scored whole by the direct
-// path (whose own guard band leads to the numpy-order ctNcc).
+// path (whose own guard band leads to the numpy-order ctNcc).  Last kernel of
+// a batch: it leaves the counters zero for the next one (the tile counts by
+// a grid-stride pass; the list's count, the item count and the queue head by
+// the workgroup that finishes last, after every workgroup has read them).
 template <int WID, int NS>
 __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t) {
     const int nfix = *t.fix_count;
     const int words = (sc.V + 63) >> 6;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += gridDim.x * 256) t.tile_count[k] = 0;
     for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
          k += gridDim.x * 4) {
         const int4 f = t.fix_list[k];
@@ -1956,6 +1731,13 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
         const int q = tx * MVS_TILE_W + (pk & 15), r = ty * MVS_TILE_H + ((pk >> 4) & 7), R = pk >> 7;
         wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * words, a.count + cand,
                             a.avg ? a.avg + cand : nullptr, a.exact_hits);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(t.done, 1) == (int)gridDim.x - 1) {
+        *t.fix_count = 0;
+        *t.n_items = 0;
+        t.tile_count[t.ntiles] = 0;   // the queue head
+        *t.done = 0;
     }
 }
 
@@ -2155,12 +1937,13 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // ---------------------------------------------------------------------------
 // The multi-GPU sweep's exchange record set (parallel.PointsExchange): the
 // accepted candidates of a rank's slice (|V| >= vlb, MVS2.py:256/369) packed
-// in index order into rows [global index, mask words..., x, y, z bits] of a
-// fixed-capacity buffer whose row 0 is the header [accepted, n, cap, 0, ...].
-// No host synchronisation: the accepted total travels in the header, and a
-// slice with more than cap accepted candidates keeps its first cap rows (the
-// receiver sees accepted > cap).  Each chunk's rows go to (sum of the earlier
-// chunks' counts) + their rank.
+// in index order into rows [global index, mask words..., (c) x, y, z as
+// binary64 bits] of a fixed-capacity buffer whose row 0 is the header
+// [accepted, n, 0...].  No host synchronisation: the accepted total travels in
+// the header, and a slice with more than cap accepted candidates keeps its
+// first cap rows (the receiver sees accepted > cap).  Each chunk's rows go to
+// (sum of the earlier chunks' counts) + their rank.  A failed look-back is
+// never silent: the header's accepted becomes -1 (PointsExchange.check raises).
 // ---------------------------------------------------------------------------
 // Chunks of kAccPer x kAccThreads candidates, thread t of a chunk holding
 // candidates chunk + t + kAccThreads j (j < kAccPer): the count reads stay
@@ -2170,28 +1953,38 @@ constexpr int kAccThreads = 256, kAccPer = 16, kAccChunk = kAccThreads * kAccPer
 // One launch: each chunk's rows start after every earlier chunk's accepted
 // count, found by a decoupled look-back over per-chunk status words
 // (epoch << 34 | flag << 32 | value; flag 1 = the chunk's own count, 2 = the
-// inclusive count through it; a word of another epoch is not yet published).
-// Workgroups are dispatched in index order and all of them fit on the chip at
-// once (<= 1024 of 256 threads), so a chunk waits only for earlier chunks'
-// workgroups, which are running; a spin limit still bounds every wait (on
-// expiry the chunk counts from 0 and *err is raised).  The words are relaxed
-// agent-scope atomics: a word carries all a reader needs, and a release or
-// acquire would write back or invalidate this XCD's L2 at every step.
+// inclusive count through it, 3 = poisoned: no valid prefix through it; a
+// word of another epoch is not yet published).  Workgroups are dispatched in
+// index order, so a chunk waits only for earlier chunks' workgroups, which
+// have started; a spin limit still bounds every wait -- a kernel sharing the
+// CUs (RCCL's, the next sweep's scorer) can delay them.  On expiry the chunk
+// counts one give-up in *err, writes no rows and publishes a poisoned word; a
+// chunk whose look-back ends on a poisoned word does the same.  The header is
+// written by the chunk that finishes last (a ticket in aux[0]; the last
+// chunk's total in aux[1]): accepted = -1 when any chunk gave up.  The words
+// are relaxed agent-scope atomics: a word carries all a reader needs, and a
+// release or acquire would write back or invalidate this XCD's L2 at every
+// step; the give-up count and the total are waited for (returning atomic /
+// s_waitcnt) before the chunk's ticket, so the last ticket sees them.
+// debug (tests only): > 0 = the spin limit; < 0 = chunk -debug gives up at once.
 constexpr int kAccGrid = 1024;
 constexpr uint32_t kAccSpin = 1u << 22;
 
 __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
-                                                          const uint64_t* __restrict__ mask, int words, int vlb, int64_t cap,
-                                                          uint64_t* __restrict__ status, uint64_t epoch,
-                                                          int32_t* __restrict__ err, int64_t* __restrict__ out) {
+                                                          const uint64_t* __restrict__ mask, const double* __restrict__ cpt,
+                                                          int words, int vlb, int64_t cap, uint64_t* __restrict__ status,
+                                                          uint64_t* __restrict__ aux, uint64_t epoch,
+                                                          int32_t* __restrict__ err, int64_t debug,
+                                                          int64_t* __restrict__ out) {
     __shared__ int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
-    __shared__ int64_t s_base;
+    __shared__ int64_t s_base;                        // -1: no valid prefix (this chunk writes no rows)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int width = 1 + words;
+    const int width = 1 + words + (cpt ? 3 : 0);
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
+    const int64_t nch = nchunk > 0 ? nchunk : 1;      // an empty slice still has chunk 0
     const uint64_t E = epoch << 34;
-    // an empty slice still has chunk 0, which writes the header
-    for (int64_t b = blockIdx.x; b < (nchunk > 0 ? nchunk : 1); b += gridDim.x) {
+    const uint32_t spin_limit = debug > 0 ? (uint32_t)debug : kAccSpin;
+    for (int64_t b = blockIdx.x; b < nch; b += gridDim.x) {
         // every load of the chunk in flight at once: the counts, then the
         // accepted candidates' first mask words
         int c[kAccPer];
@@ -2228,22 +2021,25 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             uint64_t excl = 0;
             int64_t top = b - 1;          // the window's highest chunk
             uint32_t spins = 0;
-            while (top >= 0) {
+            bool poisoned = false, gave_up = debug < 0 && b == -debug;
+            while (top >= 0 && !gave_up) {
                 const int64_t k = top - lane;
                 uint64_t v = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                     : (E | (2ull << 32));
                 const bool pub = (v & ~((1ull << 34) - 1)) == E;
                 const uint32_t flag = pub ? (uint32_t)(v >> 32) & 3u : 0u;
-                // the nearest inclusive word, and whether every chunk up to it has published
-                const uint64_t incl_m = __ballot(flag == 2), unpub = __ballot(!pub);
+                // the nearest inclusive (or poisoned) word, and whether every
+                // chunk up to it has published
+                const uint64_t incl_m = __ballot(flag >= 2), unpub = __ballot(!pub);
                 const int first_incl = incl_m ? __builtin_ctzll(incl_m) : 64;
                 const int first_unpub = unpub ? __builtin_ctzll(unpub) : 64;
                 if (first_unpub < first_incl && first_unpub < 64) {
-                    if (++spins > kAccSpin) {   // never expected: give up, count from 0
-                        if (lane == 0) atomicAdd(err, 1);
-                        break;
-                    }
+                    if (++spins > spin_limit) gave_up = true;
                     continue;                   // a chunk in the window has not published yet
+                }
+                if (first_incl < 64 && (__ballot(flag == 3) >> first_incl) & 1ull) {
+                    poisoned = true;            // the prefix through that chunk is unknown
+                    break;
                 }
                 // lanes 0..min(first_incl, 63) hold published words to sum
                 uint64_t val = (lane <= first_incl && k >= 0) ? (v & 0xffffffffull) : 0ull;
@@ -2254,32 +2050,60 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 top -= 64;
             }
             if (lane == 0) {
-                if (b > 0)
-                    __hip_atomic_store(&status[b], E | (2ull << 32) | (excl + T), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                if (b == (nchunk > 0 ? nchunk - 1 : 0)) {
-                    out[0] = (int64_t)(excl + T);   // accepted in the whole slice
-                    out[1] = n;
-                    for (int q = 2; q < width; ++q) out[q] = 0;
+                if (gave_up) {
+                    // counted (and waited for) before this chunk's ticket
+                    __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_s_waitcnt(0);
+                    poisoned = true;
                 }
-                s_base = (int64_t)excl;
+                if (b > 0)
+                    __hip_atomic_store(&status[b], E | ((poisoned ? 3ull : 2ull) << 32) | (excl + T),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (b == nch - 1) {
+                    // the slice's total for the header (-1: unknown), performed
+                    // before this chunk's ticket
+                    __hip_atomic_store(&aux[1], poisoned ? ~0ull : (excl + T), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_s_waitcnt(0);
+                }
+                s_base = poisoned ? -1 : (int64_t)excl;
             }
         }
         __syncthreads();
         const int64_t base = s_base;
+        if (base >= 0) {
 #pragma unroll
-        for (int j = 0; j < kAccPer; ++j) {
-            if ((m[j] >> lane) & 1ull) {
-                const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-                const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
-                                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
-                if (pos < cap) {
-                    int64_t* o = out + (1 + pos) * width;
-                    o[0] = offset + i;
-                    o[1] = (int64_t)w0[j];
-                    for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
+            for (int j = 0; j < kAccPer; ++j) {
+                if ((m[j] >> lane) & 1ull) {
+                    const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+                    const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
+                                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
+                    if (pos < cap) {
+                        int64_t* o = out + (1 + pos) * width;
+                        o[0] = offset + i;
+                        o[1] = (int64_t)w0[j];
+                        for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
+                        if (cpt) {
+                            // the accepted 3D point itself (binary64 bits)
+                            o[1 + words] = __double_as_longlong(cpt[3 * i]);
+                            o[2 + words] = __double_as_longlong(cpt[3 * i + 1]);
+                            o[3 + words] = __double_as_longlong(cpt[3 * i + 2]);
+                        }
+                    }
                 }
+            }
+        }
+        if (threadIdx.x == 0) {
+            // the chunk that finishes last writes the header
+            const uint64_t tk = __hip_atomic_fetch_add(&aux[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk == (uint64_t)(nch - 1)) {
+                const int gave = __hip_atomic_exchange(err, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t tot = __hip_atomic_load(&aux[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                out[0] = (gave != 0 || tot == ~0ull) ? -1 : (int64_t)tot;
+                out[1] = n;
+                for (int q = 2; q < width; ++q) out[q] = 0;
+                __hip_atomic_store(&aux[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
             }
         }
         __syncthreads();
@@ -2436,8 +2260,8 @@ int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipSt
 }
 
 template <int WID>
-int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s,
-                         hipEvent_t ev0, hipEvent_t ev1) {
+int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt,
+                         hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (a->n == 0) return 0;
     const bool grouped = sc->V > kGroupViews;
     if (t->tw != MVS_TILE_W || t->th != MVS_TILE_H || t->items == nullptr ||
@@ -2459,6 +2283,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     {
         TimedLaunch tl(s, ev0, ev1);
         if (grouped) rc = launch_mma<WID, 4, true>(sc, a, t, s);
+        else if (mt) rc = mvs_launch_score_tab(sc, a, t, mt, s);   // window moments from the scene's tables
         else switch ((sc->V + 15) / 16) {
             case 1: rc = launch_mma<WID, 1, false>(sc, a, t, s); break;
             case 2: rc = launch_mma<WID, 2, false>(sc, a, t, s); break;
@@ -2549,17 +2374,18 @@ extern "C" size_t mvs_mma_lds_bytes(int V, int wid) {
 extern "C" const char* mvs_timed_kernel_name(int V, int wid, int tiled) {
     (void)wid;
     if (!tiled) return "k_score";
+    if (tiled == 2) return "k_score_tab";
     return V > kGroupViews ? "k_score_mma_v" : "k_score_mma";
 }
 
 extern "C" int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
-                                      hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                                      const MomentsDev* mt, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     switch (wid) {
-        case 1: return launch_score_tiled_w<1>(sc, a, t, s, ev0, ev1);
-        case 2: return launch_score_tiled_w<2>(sc, a, t, s, ev0, ev1);
-        case 3: return launch_score_tiled_w<3>(sc, a, t, s, ev0, ev1);
-        case 4: return launch_score_tiled_w<4>(sc, a, t, s, ev0, ev1);
-        case 5: return launch_score_tiled_w<5>(sc, a, t, s, ev0, ev1);
+        case 1: return launch_score_tiled_w<1>(sc, a, t, mt, s, ev0, ev1);
+        case 2: return launch_score_tiled_w<2>(sc, a, t, mt, s, ev0, ev1);
+        case 3: return launch_score_tiled_w<3>(sc, a, t, mt, s, ev0, ev1);
+        case 4: return launch_score_tiled_w<4>(sc, a, t, mt, s, ev0, ev1);
+        case 5: return launch_score_tiled_w<5>(sc, a, t, mt, s, ev0, ev1);
         default: return -2;
     }
 }
@@ -2586,13 +2412,14 @@ extern "C" int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hip
 }
 
 extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask,
-                                        int words, int vlb, int64_t cap, uint64_t* status, uint64_t epoch,
-                                        int32_t* err, int64_t* out, hipStream_t s) {
+                                        const double* c, int words, int vlb, int64_t cap, uint64_t* status,
+                                        uint64_t* aux, uint64_t epoch, int32_t* err, int64_t debug, int64_t* out,
+                                        hipStream_t s) {
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, kAccGrid));
     // n == 0 still writes the header (chunk 0 of an empty slice)
-    hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, words, vlb, cap,
-                       status, epoch, err, out);
+    hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, c, words, vlb, cap,
+                       status, aux, epoch, err, debug, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

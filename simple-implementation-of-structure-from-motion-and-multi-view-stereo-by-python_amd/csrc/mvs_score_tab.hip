@@ -1,0 +1,608 @@
+// The tiled matrix-core photo test for V <= 64 with per-scene window moments
+// (gfx950 / CDNA4).
+//
+// Reference path: MyPatch.photo_consistenecy_test (MVS2.py:62-77) -> ctNcc
+// (MVS2.py:39-43) of every view's window (getDescFeatures,
+// HarrisFeatures.py:116-133) against the reference view's, all at the
+// reference view's pixel (MVS2.py:68).
+//
+// ctNcc(a, b) = n (n S_ab - S_a S_b) / ((n-1) sqrt(D_a) sqrt(D_b)),
+// D = n S_xx - S_x^2.  Everything but S_ab depends on one (pixel, view)
+// window alone, and the scene is immutable: k_moments computes S_b and
+// w_b = 1/sqrt(D_b) once per scene (and window size) into two pixel-major
+// tables, and the scorer k_score_tab only forms the window products S_ab on
+// the matrix cores (v_mfma_i32_16x16x64_i8 over the tile's staged region, as
+// k_score_mma does) and takes the decision num w_b > T from the tables.
+#include "mvs_device.h"
+#include "mvs_mma.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// k_moments: S_b and w_b of every (pixel, view) with a valid window
+// (getDescFeatures' bounds, HarrisFeatures.py:128), 32 columns x 16 rows x 16
+// views per workgroup.  The gray bytes of the block's views and rows land in
+// LDS; per (view, row) the horizontal window sums (S = sum g, Q = sum g^2 of
+// the unsigned g, packed Q << 12 | S) by a running prefix; per (view, column)
+// the vertical sums slide down the 16 rows.  The same arithmetic as the
+// in-kernel moments of k_score_mma (the tables are bit-identical to them):
+// D = n Q - S^2 (exact int32), w = v_rsq_f64(D) + one Newton step (a constant
+// window: D = 0, inf, then nan), S_b = S - 128 n.  Stores: lanes = 16 views x
+// 4 pixels, one 128-B row piece of w per pixel.
+// ---------------------------------------------------------------------------
+constexpr int kMomW = 32, kMomH = 16, kMomV = 16;
+
+template <int WID>
+__global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const MomentsDev mt) {
+    constexpr int NB = 2 * WID + 1, NPX = NB * NB;
+    constexpr int ROWS = kMomH + 2 * WID, COLS = kMomW + 2 * WID, CP = (COLS + 3) & ~3;
+    __shared__ __attribute__((aligned(16))) uint8_t g[kMomV][ROWS][CP];
+    __shared__ uint32_t hs[kMomV][ROWS][kMomW];
+    const int x0 = blockIdx.x * kMomW, y0 = blockIdx.y * kMomH, v0 = blockIdx.z * kMomV;
+    const int tid = threadIdx.x;
+    const int nv = min(kMomV, sc.V - v0);
+    // the bytes: gv rows (signed s = g - 128, 8 pad bytes left of column 0 and
+    // >= 24 right of W-1); rows outside the image clamped (never in a valid
+    // window); views past V zero
+    for (int k = tid; k < kMomV * ROWS * COLS; k += 256) {
+        const int vi = k / (ROWS * COLS), rc = k - vi * (ROWS * COLS), r = rc / COLS, c = rc - r * COLS;
+        const int y = min(max(y0 - WID + r, 0), sc.H - 1);
+        const int x = min(max(x0 - WID + c, -8), sc.W + 23);
+        g[vi][r][c] = vi < nv ? (uint8_t)(sc.gv[((int64_t)(v0 + vi) * sc.H + y) * sc.Wp + x] ^ 0x80) : (uint8_t)0;
+    }
+    __syncthreads();
+    for (int k = tid; k < kMomV * ROWS; k += 256) {
+        const int vi = k / ROWS, r = k - vi * ROWS;
+        const uint8_t* row = g[vi][r];
+        uint32_t S = 0, Q = 0;
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+            S += row[c];
+            Q += (uint32_t)row[c] * row[c];
+        }
+        hs[vi][r][0] = (Q << 12) | S;
+        for (int x = 1; x < kMomW; ++x) {
+            const uint32_t a = row[x - 1], b = row[x + NB - 1];
+            S += b - a;
+            Q += b * b - a * a;
+            hs[vi][r][x] = (Q << 12) | S;
+        }
+    }
+    __syncthreads();
+    const int x_lo = WID + 1, x_hi = sc.W - WID - 2, y_lo = WID, y_hi = sc.H - WID - 2;   // valid centres
+    for (int k = tid; k < kMomV * kMomW; k += 256) {
+        const int vi = k & (kMomV - 1), xl = k >> 4;
+        const int x = x0 + xl;
+        if (x < x_lo || x > x_hi) continue;
+        int S = 0, Q = 0;
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+            const uint32_t h = hs[vi][r][xl];
+            S += (int)(h & 0xfffu);
+            Q += (int)(h >> 12);
+        }
+        for (int yl = 0; yl < kMomH; ++yl) {
+            if (yl > 0) {
+                const uint32_t a = hs[vi][yl - 1][xl], b = hs[vi][yl + NB - 1][xl];
+                S += (int)(b & 0xfffu) - (int)(a & 0xfffu);
+                Q += (int)(b >> 12) - (int)(a >> 12);
+            }
+            const int y = y0 + yl;
+            if (y < y_lo || y > y_hi) continue;
+            const int64_t o = ((int64_t)y * sc.W + x) * mt.VP + v0 + vi;
+            if (vi < nv) {
+                const int db = NPX * Q - S * S;
+                const double D = (double)db;
+                double w = __builtin_amdgcn_rsq(D);
+                w = w * (1.5 - 0.5 * D * w * w);
+                mt.sb[o] = (int16_t)(S - 128 * NPX);
+                mt.w[o] = w;
+            } else {
+                mt.sb[o] = 0;
+                mt.w[o] = __builtin_nan("");
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_score_tab (V <= 64).  Two workgroups of 8 waves per CU (each <= 80 KiB of
+// LDS), each taking work items -- the candidates of one 16x8 pixel tile, at
+// most kMmaChunk -- from the dynamic queue k_bin's item scan built (tile
+// order).  Per item:
+//   1. the item's window region of every view (signed bytes, [view][ROWS][32],
+//      one pad row per view) and its candidate list are in LDS (LDS-DMA,
+//      double-buffered where LDS allows: item k+1's lands while item k is
+//      scored; a barrier per item);
+//   2. wave w takes the item's M-blocks [w nblk / 8, (w+1) nblk / 8) and sorts
+//      its own candidates by row pair (ballots, in its own part of the list:
+//      no workgroup barrier), so that a unit's windows span few K-steps;
+//   3. units of two M-blocks of 16 candidates: C[m][v] = sum over the window
+//      of s_R s_v by v_mfma_i32_16x16x64_i8 (A = the reference window masked
+//      to candidate m's window, B = view v's region), exact; meanwhile S_b,
+//      w_b of the unit's pixels come from the tables (global loads, one
+//      candidate step ahead of their use);
+//   4. num = n C - S_a S_b, ncc > thr <=> num w_b > T = thr (n-1)/(n w_a): one
+//      binary32 fma per (candidate, view), guard band 2e-6 |T| (k_score_fix
+//      re-scores a candidate with a pair inside it), the passing terms
+//      summed in binary64 (avg_ncc_score).
+// The other workgroup on the CU fills the issue slots this one leaves at its
+// barrier and in its latency waits.
+// ---------------------------------------------------------------------------
+constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = 512;
+constexpr int kTabChunk = MVS_MMA_CHUNK;
+
+// a candidate's constants in a unit (per wave, 32 slots)
+struct alignas(16) TabInfo {
+    int32_t tix;   // table element of its pixel, view 0
+    int32_t Sa;    // -S_a
+    int32_t R;     // reference view (-1: no candidate)
+    float T;       // decision threshold on num w_b (FAST)
+};
+
+template <int WID, int NBLK>
+struct TabGeom {
+    static constexpr int VP = 16 * NBLK;
+    static constexpr int RB = VP * MmaGeom<WID>::VS;    // one region buffer (+16 zero bytes)
+    static constexpr int CB = kTabChunk * 8;            // one candidate buffer
+    static constexpr int FIXED = kTabWaves * 32 * (int)sizeof(TabInfo) + 65 * 8 + 64;
+    // two buffers of each where two workgroups per CU still fit (80 KiB each)
+    static constexpr bool DB = 2 * (RB + 16) + 2 * CB + FIXED <= 80 * 1024 - 512;
+};
+
+template <int WID, int NBLK, bool FAST>
+__global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
+                                                               const MomentsDev mt, const int4* __restrict__ items,
+                                                               const int2* __restrict__ sorted) {
+    using G = MmaGeom<WID>;
+    using TG = TabGeom<WID, NBLK>;
+    constexpr int NB = G::NB, NPX = G::NPX, KS = G::KS, VS = G::VS, C0 = G::C0;
+    constexpr int VP = TG::VP;
+    constexpr bool DB = TG::DB;
+    constexpr int RPV = VS / 32;                                          // region rows per view incl. the pad row
+    constexpr int PF = (VP * RPV * 2 + kTabThreads - 1) / kTabThreads;    // 16-B pieces per thread
+    constexpr int RB = TG::RB, CB = TG::CB;
+    // distinct LDS objects per buffer: reads of one do not wait for the
+    // LDS-DMA into the other; each region buffer ends in 16 zero bytes (rows
+    // outside a window read them by an offset select inside the same buffer)
+    __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB + 16], s_reg1[DB ? RB + 16 : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[DB ? CB : 16];
+    __shared__ __attribute__((aligned(16))) TabInfo s_ti[kTabWaves * 32];
+    __shared__ int s_ids[2];
+    __shared__ double s_recip[65];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int V = sc.V;
+    const int npiece = V * RPV * 2;
+    if (tid <= 64) s_recip[tid] = c_recip.r[tid];
+    if (tid < 4) ((uint32_t*)(s_reg0 + RB))[tid] = 0u;
+    if (DB && tid >= 4 && tid < 8) ((uint32_t*)(s_reg1 + RB))[tid & 3] = 0u;
+    TabInfo* ti = s_ti + wave * 32;
+
+    const double kn = (double)NPX / (double)(NPX - 1);
+    const float tqf = (float)(a.thr / kn);
+    const int n_units = *t.n_items;
+    int32_t* head = &t.tile_count[t.ntiles];
+    const int16_t* __restrict__ tsb = mt.sb;
+    const double* __restrict__ tw = mt.w;
+
+    auto region_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_reg1 : s_reg0; };
+    auto cand_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_cand1 : s_cand0; };
+    // the item's region (gv rows) and sorted (id, pk) entries by LDS-DMA
+    auto stage = [&](const int4 d, auto bufc) {
+        const int ty = d.x / t.ntx, tx = d.x - ty * t.ntx;
+        const int x0 = tx * MVS_TILE_W, yr0 = ty * MVS_TILE_H - WID;
+        uint8_t* base = region_buf(bufc);
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int k = tid + p * kTabThreads;
+            if (k < npiece) {
+                const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
+                const int y = min(max(yr0 + (r2 >> 1), 0), sc.H - 1);
+                const uint8_t* src = sc.gv + ((int64_t)v * sc.H + y) * sc.Wp + (x0 - 8) + 16 * (r2 & 1);
+                __builtin_amdgcn_global_load_lds((const void*)src,
+                                                 (void __attribute__((address_space(3)))*)(base + (p * kTabThreads + wave * 64) * 16),
+                                                 16, 0, 0);
+            }
+        }
+        uint8_t* cbase = cand_buf(bufc);
+        const int32_t* csrc = (const int32_t*)(sorted + d.y);
+#pragma unroll
+        for (int p = 0; p < 2 * kTabChunk / kTabThreads; ++p) {
+            const int k = tid + p * kTabThreads;
+            if (k < 2 * d.z)
+                __builtin_amdgcn_global_load_lds((const void*)(csrc + k),
+                                                 (void __attribute__((address_space(3)))*)(cbase + (p * kTabThreads + wave * 64) * 4),
+                                                 4, 0, 0);
+        }
+    };
+
+    // the item pipeline: while item k is scored, item k+1's region and list
+    // (DB), item k+2's descriptor and thread 0's claim of item k+3 are in flight
+    if (tid == 0) {
+        s_ids[0] = atomicAdd(head, 1);
+        s_ids[1] = atomicAdd(head, 1);
+    }
+    __syncthreads();
+    int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
+    int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
+    if (cur >= n_units) return;
+    int4 dcur = item_desc(t, items, cur);
+    dcur = make_int4(__builtin_amdgcn_readfirstlane(dcur.x), __builtin_amdgcn_readfirstlane(dcur.y),
+                     __builtin_amdgcn_readfirstlane(dcur.z), 0);
+    stage(dcur, std::integral_constant<int, 0>{});
+    int4 dnx1 = nx1 < n_units ? item_desc(t, items, nx1) : make_int4(0, 0, 0, 0);
+    int pend = 0;
+    if (tid == 0) pend = atomicAdd(head, 1);
+    __syncthreads();   // everyone has read s_ids before they are rewritten
+
+    auto round = [&](auto bufc) -> bool {
+        constexpr int buf = decltype(bufc)::value;
+        const int nc = dcur.z;
+        const uint8_t* reg = region_buf(bufc);
+        int2* cand = (int2*)cand_buf(bufc);
+        const int zoff = RB;   // the zero row, relative to the region buffer
+        // ---- 1. this item's region and list have landed (every wave's DMA) ----
+        if (tid == 0) s_ids[0] = pend;
+        __syncthreads();
+        const int nx2 = __builtin_amdgcn_readfirstlane(s_ids[0]);
+        // the next item's region and list into the other buffer, the descriptor
+        // after it, thread 0's claim of the one after that
+        if constexpr (DB) {
+            if (nx1 < n_units) stage(dnx1, std::integral_constant<int, buf ^ 1>{});
+        }
+        int4 dnx2 = make_int4(0, 0, 0, 0);
+        if (nx2 < n_units) {
+            dnx2 = item_desc(t, items, nx2);
+            if (tid == 0) pend = atomicAdd(head, 1);
+        }
+        const int ty = dcur.x / t.ntx, tx = dcur.x - ty * t.ntx;
+        const int tix0 = ((ty * MVS_TILE_H) * sc.W + tx * MVS_TILE_W) * VP;   // table element of the tile origin
+        // ---- 2. this wave's M-blocks, sorted by row pair inside the wave ----
+        const int nblk = (nc + 15) >> 4;
+        const int b0 = (nblk * wave) >> 3, b1 = (nblk * (wave + 1)) >> 3;
+        {
+            const int base = 16 * b0, cnt = min(16 * b1, nc) - base;   // <= 128
+            int2 c0 = make_int2(0, 0), c1 = make_int2(0, 0);
+            int bin0 = 4, bin1 = 4;
+            if (lane < cnt) { c0 = cand[base + lane]; bin0 = (c0.y >> 5) & 3; }
+            if (lane + 64 < cnt) { c1 = cand[base + 64 + lane]; bin1 = (c1.y >> 5) & 3; }
+            int r0 = 0, r1 = 0, run = 0;
+            static_for<4>([&](auto Yc) {
+                constexpr int y = Yc;
+                const uint64_t m0 = __ballot(bin0 == y), m1 = __ballot(bin1 == y);
+                const int p0 = __popcll(m0);
+                if (bin0 == y) r0 = run + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+                if (bin1 == y) r1 = run + p0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+                run += p0 + __popcll(m1);
+            });
+            if (lane < cnt) cand[base + r0] = c0;
+            if (lane + 64 < cnt) cand[base + r1] = c1;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        // ---- 3. + 4. units of two M-blocks (32 consecutive sorted candidates) ----
+        for (int fb = b0; fb < b1; fb += 2) {
+            const int nh = min(2, b1 - fb);
+            auto unit = [&](auto nhc) {
+                constexpr int NH = decltype(nhc)::value;
+                const int ol = opaque(lane);
+                const int m = ol & 15, kh = ol >> 4;
+                int2 e[NH];
+                bool valid[NH];
+                int qrel[NH], rrel[NH], Rv[NH];
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    const int kk = (fb + h) * 16 + m;
+                    valid[h] = kk < nc;
+                    e[h] = valid[h] ? cand[kk] : make_int2(-1, 0);
+                    qrel[h] = e[h].y & 15;
+                    rrel[h] = (e[h].y >> 4) & 7;
+                    Rv[h] = e[h].y >> 7;
+                }
+                // row 0 of the wave: each candidate's table row, published for
+                // the epilogue's lanes; its own S_a and w_a from the tables
+                int sa_raw[NH];
+                double wa_raw[NH];
+#pragma unroll
+                for (int h = 0; h < NH; ++h) { sa_raw[h] = 0; wa_raw[h] = 0.0; }
+                if (kh == 0) {
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        const int tix = tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
+                        ti[16 * h + m].tix = tix;
+                        ti[16 * h + m].R = valid[h] ? Rv[h] : -1;
+                        sa_raw[h] = tsb[tix + Rv[h]];
+                        wa_raw[h] = tw[tix + Rv[h]];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // the epilogue's table values, one candidate step ahead: lane
+                // (kh, m) needs candidate 4 kh + i's S_b and w_b of views 16 nb + m
+                int sbv[2][NH][NBLK];
+                double wv[2][NH][NBLK];
+                auto fetch = [&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        const int tix = ti[16 * h + 4 * kh + i].tix + m;
+#pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) {
+                            sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
+                            wv[i & 1][h][nb] = tw[tix + 16 * nb];
+                        }
+                    }
+                };
+                // the unit's candidates are sorted by row pair: its window rows lie
+                // in candidate 0's pair to the last valid candidate's pair + NB - 1
+                const int last = min(16 * NH - 1, nc - 1 - fb * 16);
+                const int r_lo = __builtin_amdgcn_readlane(rrel[0], 0) & ~1;
+                const int r_hi = (last >= 16 ? __builtin_amdgcn_readlane(rrel[NH - 1], last - 16)
+                                             : __builtin_amdgcn_readlane(rrel[0], last)) | 1;
+                constexpr int KSK = WID + 1;     // K-steps of one row's windows
+                const int s_lo = r_lo >> 1, s_hi = (r_hi + NB - 1) >> 1;
+                const int span = s_hi - s_lo + 1;
+                // A: the reference windows, masked to each candidate's window
+                // columns (this lane's 16 columns) and rows (bit 2s: K-step s holds
+                // a window row of this lane's row parity)
+                uint32_t cm[NH][4], rb[NH];
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    const uint32_t wm = valid[h] ? (((1u << NB) - 1u) << (qrel[h] + C0)) : 0u;
+                    const uint32_t hm = wm >> (16 * (kh & 1));
+#pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) cm[h][k4] = byte_mask((hm >> (4 * k4)) & 15u);
+                    rb[h] = valid[h] ? (((1u << NB) - 1u) << rrel[h]) >> (kh >> 1) : 0u;
+                }
+                const int lofs = 32 * (kh >> 1) + 16 * (kh & 1);
+                v4i C[NH][NBLK];
+#pragma unroll
+                for (int h = 0; h < NH; ++h)
+#pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) C[h][nb] = (v4i){0, 0, 0, 0};
+                // NST K-steps from sb; steps below sd are done (their A rows read
+                // zeros); steps [SAFE_LO, SAFE_HI] hold window rows of every
+                // candidate of the unit (no row test there)
+                auto kpass = [&](auto nstc, auto safe_lo_c, auto safe_hi_c, int sb, int sd) {
+                    constexpr int NST = decltype(nstc)::value;
+                    constexpr int SAFE_LO = decltype(safe_lo_c)::value, SAFE_HI = decltype(safe_hi_c)::value;
+                    uint32_t rbp[NH];
+                    int aoff[NH];
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        rbp[h] = (rb[h] & ~((1u << (2 * sd)) - 1u)) >> (2 * sb);
+                        aoff[h] = Rv[h] * VS + lofs + 64 * sb;
+                    }
+                    const uint8_t* bptr[NBLK];
+#pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) bptr[nb] = reg + min(16 * nb + m, V - 1) * VS + lofs + 64 * sb;
+                    uint4 av[2][NH], bv[2][NBLK];
+                    auto load = [&](int st, int slot) {
+#pragma unroll
+                        for (int h = 0; h < NH; ++h)
+                            av[slot][h] = *(const uint4*)(reg + ((st >= SAFE_LO && st <= SAFE_HI) ||
+                                                                         ((rbp[h] >> (2 * st)) & 1u)
+                                                                     ? aoff[h] + 64 * st : zoff));
+#pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) bv[slot][nb] = *(const uint4*)(bptr[nb] + 64 * st);
+                    };
+                    load(0, 0);
+#pragma unroll
+                    for (int st = 0; st < NST; ++st) {
+                        const int cs = st & 1;
+                        if (st + 1 < NST) load(st + 1, cs ^ 1);
+                        v4i A[NH];
+#pragma unroll
+                        for (int h = 0; h < NH; ++h)
+                            A[h] = (v4i){(int)(av[cs][h].x & cm[h][0]), (int)(av[cs][h].y & cm[h][1]),
+                                         (int)(av[cs][h].z & cm[h][2]), (int)(av[cs][h].w & cm[h][3])};
+#pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) {
+                            const v4i B = {(int)bv[cs][nb].x, (int)bv[cs][nb].y, (int)bv[cs][nb].z, (int)bv[cs][nb].w};
+#pragma unroll
+                            for (int h = 0; h < NH; ++h)
+                                C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[h], B, C[h][nb], 0, 0, 0);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                };
+                using I = std::integral_constant<int, 0>;
+                if (span <= KSK) {
+                    kpass(std::integral_constant<int, KSK>{}, std::integral_constant<int, 1>{},
+                          std::integral_constant<int, KSK - 2>{}, min(s_lo, KS - KSK), 0);
+                } else if (span == KSK + 1) {
+                    kpass(std::integral_constant<int, KSK + 1>{}, std::integral_constant<int, 2>{},
+                          std::integral_constant<int, KSK - 2>{}, min(s_lo, KS - KSK - 1), 0);
+                } else {
+                    for (int sd = s_lo; sd <= s_hi; sd += KSK)
+                        kpass(std::integral_constant<int, KSK>{}, std::integral_constant<int, KSK>{}, I{},
+                              min(sd, KS - KSK), sd);
+                }
+                // the first candidate step's table values (issued after the K-loop:
+                // in flight across it they would hold 18 registers)
+                fetch(std::integral_constant<int, 0>{});
+                // the candidates' decision constants (row 0), now that S_a, w_a are in
+                double my_wa[NH];
+#pragma unroll
+                for (int h = 0; h < NH; ++h) my_wa[h] = 0.0;
+                if (kh == 0) {
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        const double wa = wa_raw[h];
+                        ti[16 * h + m].Sa = -sa_raw[h];
+                        // FAST: T = thr (n-1)/n sqrt(da) in binary32 (1-ulp reciprocal,
+                        // well inside the guard band); else the decision is on ncc
+                        ti[16 * h + m].T = FAST ? (valid[h] ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf(""))
+                                                : 0.0f;
+                        my_wa[h] = wa;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // lane (kh, m) holds C[h][nb][i] = block h's candidate 4 kh + i, view 16 nb + m
+                uint32_t pmv[NH], gdv[NH];
+#pragma unroll
+                for (int h = 0; h < NH; ++h) pmv[h] = gdv[h] = 0u;
+                double sacc[NH][4];
+                static_for<4>([&](auto Ic) {
+                    constexpr int i = Ic;
+                    if constexpr (i < 3) fetch(std::integral_constant<int, i + 1>{});
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        const TabInfo c = ti[16 * h + 4 * kh + i];
+                        const float gT = 2e-6f * fabsf(c.T);
+                        double ca = 0.0;
+                        if constexpr (!FAST) ca = c.R < 0 ? 0.0 : kn * tw[c.tix + c.R];
+                        double sa = 0.0;
+                        uint64_t g = 0;
+                        float ax[NBLK];
+                        static_for<NBLK>([&](auto Nc) {
+                            constexpr int nb = Nc;
+                            const int vl = 16 * nb + m;
+                            const int num = __mul24(c.Sa, sbv[i & 1][h][nb]) + __mul24(NPX, C[h][nb][i]);
+                            const double w = wv[i & 1][h][nb];
+                            uint64_t P;
+                            if constexpr (FAST) {
+                                // ncc > thr <=> num w_b > T; a constant window (w_b nan)
+                                // never passes.  The candidate's own view R passes (its ncc
+                                // is n/(n-1) > thr): its mask bit and its term of the sum
+                                // are taken out once per candidate
+                                const float x = fmaf((float)num, (float)w, -c.T);
+                                P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
+                                ax[nb] = x;
+                                sa = fma_f64_lanes(sa, num, w, P);
+                            } else {
+                                const double ncc = (double)num * w * ca;
+                                const bool pass = vl != c.R && ncc > a.thr;
+                                P = __ballot(pass);
+                                g |= __ballot(vl != c.R && fabs(ncc - a.thr) <= kGuard);
+                                sa = fma((double)num, pass ? w : 0.0, sa);
+                            }
+                            pmv[h] = writelane<2 * (i * NBLK + nb)>(pmv[h], (uint32_t)P);
+                            pmv[h] = writelane<2 * (i * NBLK + nb) + 1>(pmv[h], (uint32_t)(P >> 32));
+                        });
+                        if constexpr (FAST) {
+                            float mn = fabsf(ax[0]);
+#pragma unroll
+                            for (int nb = 1; nb < NBLK; ++nb) mn = fminf(mn, fabsf(ax[nb]));
+                            g = __builtin_amdgcn_fcmpf(mn, gT, 4);                               // olt
+                        }
+                        gdv[h] = writelane<2 * i>(gdv[h], (uint32_t)g);
+                        gdv[h] = writelane<2 * i + 1>(gdv[h], (uint32_t)(g >> 32));
+                        sacc[h][i] = sa;
+                    }
+                });
+                // owner lane c = 4 j + i (row 0) of each block's candidate c: its mask
+                // bits, guard bits and sum from the lanes that hold them
+                const int jj = m >> 2, ii = m & 3;
+#pragma unroll
+                for (int h = 0; h < NH; ++h) {
+                    uint64_t mk = 0;
+#pragma unroll
+                    for (int nb = 0; nb < NBLK; ++nb) {
+                        const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (2 * (ii * NBLK + nb) + (jj >> 1)), (int)pmv[h]);
+                        mk |= (uint64_t)((d >> (16 * (jj & 1))) & 0xffffu) << (16 * nb);
+                    }
+                    const uint32_t gw = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (2 * ii + (jj >> 1)), (int)gdv[h]);
+                    const bool gg = ((gw >> (16 * (jj & 1))) & 0xffffu) != 0u;
+                    double mine = 0.0;
+                    if (a.avg != nullptr) {
+                        const double rs = row_sum16_x4(sacc[h], m);
+                        const int src = 4 * (16 * jj + ii);   // lane 16 j + i holds candidate 4 j + i's sum
+                        const unsigned long long rb64 = __double_as_longlong(rs);
+                        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)rb64);
+                        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(rb64 >> 32));
+                        mine = __longlong_as_double(((unsigned long long)hi << 32) | lo);
+                    }
+                    if (kh == 0 && valid[h]) {
+                        // the reference view itself is no V entry (MVS2.py:66-67)
+                        const uint64_t self = (mk >> Rv[h]) & 1ull;
+                        mk &= ~(1ull << Rv[h]);
+                        const int cnt = __popcll(mk);
+                        const int64_t idx = e[h].x;
+                        a.mask[idx] = mk;
+                        a.count[idx] = cnt;
+                        if (a.avg) {
+                            // its own term num_RR w_a = D_a w_a = 1 / w_a leaves the sum
+                            double inv = __builtin_amdgcn_rcp(my_wa[h]);
+                            inv = inv * (2.0 - my_wa[h] * inv);
+                            const double sum = self ? mine - inv : mine;
+                            a.avg[idx] = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
+                        }
+                        if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
+                    }
+                }
+            };
+            if (nh == 2) unit(std::integral_constant<int, 2>{});
+            else unit(std::integral_constant<int, 1>{});
+        }
+        if (nx1 >= n_units) return false;
+        if constexpr (!DB) {
+            // one buffer: every wave is done with it before the next item lands
+            __syncthreads();
+            stage(dnx1, std::integral_constant<int, 0>{});
+        }
+        cur = nx1;
+        dcur = dnx1;
+        nx1 = nx2;
+        dnx1 = dnx2;
+        return true;
+    };
+    for (;;) {
+        if (!round(std::integral_constant<int, 0>{})) break;
+        if (!round(std::integral_constant<int, DB ? 1 : 0>{})) break;
+    }
+}
+
+// hipFuncAttributeMaxDynamicSharedMemorySize is not needed: all LDS is static
+template <int WID, int NBLK>
+int launch_tab(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt, hipStream_t s) {
+    if (fabs(a->thr) >= 0.01)
+        hipLaunchKernelGGL((k_score_tab<WID, NBLK, true>), dim3(kTabGrid), dim3(kTabThreads), 0, s, *sc, *a, *t, *mt,
+                           (const int4*)t->items, (const int2*)t->sorted);
+    else
+        hipLaunchKernelGGL((k_score_tab<WID, NBLK, false>), dim3(kTabGrid), dim3(kTabThreads), 0, s, *sc, *a, *t, *mt,
+                           (const int4*)t->items, (const int2*)t->sorted);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int WID>
+int launch_tab_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt, hipStream_t s) {
+    switch ((sc->V + 15) / 16) {
+        case 1: return launch_tab<WID, 1>(sc, a, t, mt, s);
+        case 2: return launch_tab<WID, 2>(sc, a, t, mt, s);
+        case 3: return launch_tab<WID, 3>(sc, a, t, mt, s);
+        default: return launch_tab<WID, 4>(sc, a, t, mt, s);
+    }
+}
+
+}  // namespace
+
+extern "C" int mvs_launch_moments(const SceneDev* sc, const MomentsDev* mt, hipStream_t s) {
+    if (sc->V > 64 || mt->VP != 16 * ((sc->V + 15) / 16)) return -3;
+    const dim3 grid((unsigned)((sc->W + kMomW - 1) / kMomW), (unsigned)((sc->H + kMomH - 1) / kMomH),
+                    (unsigned)(mt->VP / kMomV));
+    switch (mt->wid) {
+        case 1: hipLaunchKernelGGL(k_moments<1>, grid, dim3(256), 0, s, *sc, *mt); break;
+        case 2: hipLaunchKernelGGL(k_moments<2>, grid, dim3(256), 0, s, *sc, *mt); break;
+        case 3: hipLaunchKernelGGL(k_moments<3>, grid, dim3(256), 0, s, *sc, *mt); break;
+        case 4: hipLaunchKernelGGL(k_moments<4>, grid, dim3(256), 0, s, *sc, *mt); break;
+        case 5: hipLaunchKernelGGL(k_moments<5>, grid, dim3(256), 0, s, *sc, *mt); break;
+        default: return -2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mvs_launch_score_tab(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt,
+                                    hipStream_t s) {
+    if (sc->V > 64 || t->chunk != kTabChunk) return -3;
+    switch (mt->wid) {
+        case 1: return launch_tab_w<1>(sc, a, t, mt, s);
+        case 2: return launch_tab_w<2>(sc, a, t, mt, s);
+        case 3: return launch_tab_w<3>(sc, a, t, mt, s);
+        case 4: return launch_tab_w<4>(sc, a, t, mt, s);
+        case 5: return launch_tab_w<5>(sc, a, t, mt, s);
+        default: return -2;
+    }
+}

@@ -8,11 +8,12 @@ no communication while scoring.  Two exchanges:
 
 * PointsExchange -- the bench's per-sweep exchange: each rank's accepted
   candidates (|V| >= vlb, MVS2.py:256/369) as rows [global index, mask
-  words] (16 B at V <= 64: a candidate's geometry is a function of its
-  global index, regenerated by whichever rank needs it, as in the sharded
-  stage) packed on the device (mvs_pack_accepted, no host sync) into a
-  fixed-capacity buffer and all-gathered on a communication stream while
-  the next sweep scores (double-buffered).
+  words, x, y, z] (40 B at V <= 64: the accepted 3D point itself; or 16 B
+  without the point, a candidate's geometry then being regenerated from its
+  global index as in the sharded stage) packed on the device
+  (mvs_pack_accepted, no host sync) into a fixed-capacity buffer and
+  all-gathered on a communication stream while the next sweep scores
+  (double-buffered).
 * stage_sharded -- the whole DensePointsWithMVS2 stage: every rank computes
   the geometry of every child of a sweep (it depends only on records every
   rank holds), scores its contiguous slice, and the slices' photo-test masks
@@ -30,15 +31,17 @@ def shard_range(n, rank, world):
     return begin, begin + base + (1 if rank < extra else 0)
 
 
-def points_width(words):
-    """int64 columns of an exchange row: global index, mask words."""
-    return 1 + words
+def points_width(words, points=True):
+    """int64 columns of an exchange row: global index, mask words, and the
+    accepted 3D point's x, y, z (binary64 bits) when points."""
+    return 1 + words + (3 if points else 0)
 
 
-def pack_accepted_reference(offset, count, mask, vlb, out):
+def pack_accepted_reference(offset, count, mask, vlb, out, c=None):
     """mvs_pack_accepted's layout from torch ops, for CPU tensors only (the
     gloo process groups of the CPU tests): header [accepted, n, 0...], then
-    up to cap rows in index order.  Device tensors never come here."""
+    up to cap rows in index order (with c: the points' bits after the mask
+    words).  Device tensors never come here."""
     if count.is_cuda:
         raise RuntimeError("pack_accepted_reference is for CPU tensors; device slices use mvs_pack_accepted")
     cap = out.shape[0] - 1
@@ -51,26 +54,31 @@ def pack_accepted_reference(offset, count, mask, vlb, out):
     k = idx.numel()
     out[1:1 + k, 0] = idx + offset
     out[1:1 + k, 1:1 + words] = mask[idx].view(torch.int64)
+    if c is not None:
+        out[1:1 + k, 1 + words:4 + words] = c[idx].contiguous().view(torch.int64)
 
 
 class PointsExchange:
     """Per-sweep all-gather of the accepted points as
-    [global index, mask words] rows (the 3D point follows from the index),
-    pipelined: post() packs this rank's accepted rows on the scoring stream
-    (no host sync) and starts the all-gather on a communication stream that
-    waits only for that pack, so the next sweep scores while it runs.  The
-    two send / receive buffers alternate; a pack waits for the all-gather that
-    used its buffer two sweeps before.  cap = rows per rank (the bench takes
-    the first sweep's accepted count plus a margin); a rank with more than cap
-    accepted candidates shows it in its header (check() raises).
+    [global index, mask words, x, y, z] rows (points=False: without the
+    point, which then follows from the index), pipelined: post() packs this
+    rank's accepted rows on the scoring stream (no host sync) and starts the
+    all-gather on a communication stream that waits only for that pack, so
+    the next sweep scores while it runs.  The two send / receive buffers
+    alternate; a pack waits for the all-gather that used its buffer two
+    sweeps before.  cap = rows per rank (the bench takes the first sweep's
+    accepted count plus a margin); a rank with more than cap accepted
+    candidates, or whose pack failed (header -1), shows it in its header
+    (check() and result() raise).
 
     ctx = the rank's MvsContext (its pack kernel); on CPU tensors (gloo) the
     torch reference pack is used and the all-gather is synchronous."""
 
-    def __init__(self, ctx, words, cap, device, group=None):
+    def __init__(self, ctx, words, cap, device, group=None, points=True):
         self.ctx, self.words, self.cap, self.group = ctx, words, int(cap), group
+        self.points = bool(points)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.width = points_width(words)
+        self.width = points_width(words, self.points)
         self.device = torch.device(device)
         cuda = self.device.type == "cuda"
         self.send = [torch.zeros((self.cap + 1, self.width), dtype=torch.int64, device=device) for _ in range(2)]
@@ -80,9 +88,13 @@ class PointsExchange:
         self.done = [None, None]
         self.posted = 0
 
-    def post(self, offset, count, mask, vlb, stream=None):
-        """Pack this rank's accepted rows of a scored slice and start the
-        all-gather; returns the buffer index for result()."""
+    def post(self, offset, count, mask, vlb, stream=None, c=None):
+        """Pack this rank's accepted rows of a scored slice (c: its (n, 3)
+        float64 centres, required when points) and start the all-gather;
+        returns the buffer index for result()."""
+        if self.points and c is None:
+            raise RuntimeError("PointsExchange(points=True).post needs the slice's centres c")
+        cc = c if self.points else None
         b = self.posted & 1
         self.posted += 1
         if count.is_cuda:
@@ -93,11 +105,12 @@ class PointsExchange:
                 raise RuntimeError("PointsExchange.post needs a non-default stream")
             if self.done[b] is not None:
                 cur.wait_event(self.done[b])          # the all-gather two sweeps back has read send[b]
-            self.ctx.pack_accepted(offset, count, mask, vlb, self.send[b], stream=cur.cuda_stream)
-            if self.world == 1:
-                return b
+            self.ctx.pack_accepted(offset, count, mask, vlb, self.send[b], stream=cur.cuda_stream, c=cc)
             packed = torch.cuda.Event()
             packed.record(cur)
+            if self.world == 1:
+                self.done[b] = packed                 # result()/check() wait for the pack itself
+                return b
             with torch.cuda.stream(self.comm):
                 self.comm.wait_event(packed)
                 work = dist.all_gather_into_tensor(self.recv[b], self.send[b], group=self.group, async_op=True)
@@ -106,7 +119,7 @@ class PointsExchange:
                 ev.record(self.comm)
             self.done[b] = ev
             return b
-        pack_accepted_reference(offset, count, mask, vlb, self.send[b])
+        pack_accepted_reference(offset, count, mask, vlb, self.send[b], cc)
         if self.world > 1:
             dist.all_gather_into_tensor(self.recv[b], self.send[b], group=self.group)
         return b
@@ -124,21 +137,33 @@ class PointsExchange:
     def result(self, b):
         """The gathered accepted rows of every rank, concatenated in rank order
         (host sync; a consumer of the exchange, not the timed loop):
-        (global index, mask (k, words) int64 view)."""
+        (global index, mask (k, words) int64 view[, points (k, 3) float64])."""
+        blk = self.check(b)
+        rows = torch.cat([blk[r, 1:1 + int(blk[r, 0, 0])] for r in range(blk.shape[0])])
+        if self.points:
+            pts = rows[:, 1 + self.words:4 + self.words].contiguous().view(torch.float64)
+            return rows[:, 0], rows[:, 1:1 + self.words], pts
+        return rows[:, 0], rows[:, 1:1 + self.words]
+
+    def check(self, b=None):
+        """Wait for buffer b's exchange (default: the last posted) and raise if
+        any rank's pack failed (header -1) or accepted more candidates than the
+        capacity; -> the (world, cap + 1, width) gathered block."""
+        b = (self.posted - 1) & 1 if b is None else b
         if self.done[b] is not None:
             self.done[b].synchronize()
         blk = self.blocks(b)
-        self.check(blk)
-        rows = torch.cat([blk[r, 1:1 + int(blk[r, 0, 0])] for r in range(blk.shape[0])])
-        return rows[:, 0], rows[:, 1:1 + self.words]
-
-    def check(self, blk=None):
-        """Raise if any rank accepted more candidates than the capacity."""
-        blk = self.blocks((self.posted - 1) & 1) if blk is None else blk
         acc = blk[:, 0, 0].tolist()
+        if min(acc) < 0:
+            raise RuntimeError(f"PointsExchange: the device pack of rank(s) "
+                               f"{[r for r, a in enumerate(acc) if a < 0]} failed (look-back gave up)")
         if max(acc) > self.cap:
             raise RuntimeError(f"PointsExchange capacity {self.cap} < accepted {max(acc)}")
-        return acc
+        return blk
+
+    def accepted(self, b=None):
+        """Accepted rows per rank of buffer b (after check())."""
+        return self.check(b)[:, 0, 0].tolist()
 
 
 def gather_slices(out, group=None):

@@ -274,9 +274,11 @@ def test_timed_kernel_name(ctx, dino):
 def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     """mvs_pack_accepted (the multi-GPU exchange's device pack, no host sync)
     against parallel.pack_accepted_reference on the bench's 2^20 sweep:
-    identical header and rows, including a capacity below the accepted count
-    (the first cap rows, the true count in the header) and an empty slice.
-    The pack's device time is printed (budget: <= 10 us per 2^20 sweep)."""
+    identical header and rows -- with the accepted 3D points (40-B rows, the
+    bench's exchange) and without (16-B rows) -- including a capacity below the
+    accepted count (the first cap rows, the true count in the header) and an
+    empty slice.  The pack's device time is printed (budget: <= 10 us per 2^20
+    sweep for the 16-B rows)."""
     import importlib
     import torch
     par = importlib.import_module(pkg.__name__ + ".parallel")
@@ -292,39 +294,48 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     torch.cuda.synchronize()
     acc = int((count >= 3).sum())
     assert acc > 1000
-    for cap, off in ((acc + 300, 5 << 20), (acc // 3, 0)):
-        out = torch.full((cap + 1, 2), -9, dtype=torch.int64, device=dev)
-        torch.cuda.synchronize()
-        ctx.pack_accepted(off, count, mask, 3, out)   # the library's stream
-        torch.cuda.synchronize()
-        exp = torch.full((cap + 1, 2), -9, dtype=torch.int64)
-        par.pack_accepted_reference(off, count.cpu(), mask.cpu(), 3, exp)
-        got = out.cpu()
-        k = min(acc, cap)
-        assert got[0].tolist() == [acc, n]
-        assert torch.equal(got[1:1 + k], exp[1:1 + k])
+    for pts in (False, True):
+        w = par.points_width(1, pts)
+        for cap, off in ((acc + 300, 5 << 20), (acc // 3, 0)):
+            out = torch.full((cap + 1, w), -9, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            ctx.pack_accepted(off, count, mask, 3, out, c=tc if pts else None)   # the library's stream
+            torch.cuda.synchronize()
+            exp = torch.full((cap + 1, w), -9, dtype=torch.int64)
+            par.pack_accepted_reference(off, count.cpu(), mask.cpu(), 3, exp, torch.from_numpy(c) if pts else None)
+            got = out.cpu()
+            k = min(acc, cap)
+            assert got[0].tolist() == [acc, n] + [0] * (w - 2)
+            assert torch.equal(got[1:1 + k], exp[1:1 + k])
+            if pts:   # the rows carry the candidates' own centres, bit for bit
+                idx = got[1:1 + k, 0].numpy() - off
+                assert np.array_equal(got[1:1 + k, 2:5].contiguous().view(torch.float64).numpy(), c[idx])
     empty = torch.full((4, 2), -9, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     ctx.pack_accepted(0, count[:0], mask[:0], 3, empty)
     torch.cuda.synchronize()
     assert empty[0].cpu().tolist() == [0, 0]
-    out = torch.empty((acc + 300 + 1, 2), dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream()
-    for _ in range(3):
-        ctx.pack_accepted(0, count, mask, 3, out, stream=s.cuda_stream)
-    # the packs queue behind scoring work, so that the events time the device
-    # and not the host's submission rate (~15 us per ctypes call + 2 launches)
-    for _ in range(3):
-        ctx.score_device(tc, tr, xy, mask, count, None, 0.7, 5, stream=s.cuda_stream)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(20):
-        ctx.pack_accepted(0, count, mask, 3, out, stream=s.cuda_stream)
-    e1.record(s)
-    e1.synchronize()
-    us = e0.elapsed_time(e1) / 20 * 1e3
-    print(f"pack_accepted: {us:.1f} us per 2^20 sweep ({acc} accepted rows)")
-    assert us <= 10.0
+    for pts in (False, True):
+        out = torch.empty((acc + 300 + 1, par.points_width(1, pts)), dtype=torch.int64, device=dev)
+        cc = tc if pts else None
+        for _ in range(3):
+            ctx.pack_accepted(0, count, mask, 3, out, stream=s.cuda_stream, c=cc)
+        # the packs queue behind scoring work, so that the events time the device
+        # and not the host's submission rate (~15 us per ctypes call + 2 launches)
+        for _ in range(3):
+            ctx.score_device(tc, tr, xy, mask, count, None, 0.7, 5, stream=s.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(20):
+            ctx.pack_accepted(0, count, mask, 3, out, stream=s.cuda_stream, c=cc)
+        e1.record(s)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1e3
+        print(f"pack_accepted ({'40' if pts else '16'}-B rows): {us:.1f} us per 2^20 sweep ({acc} accepted rows)")
+        assert int(out[0, 0]) == acc
+        if not pts:
+            assert us <= 10.0
 
 
 @pytest.mark.parametrize("n", [1, 4095, 4097, 5_000_001])
@@ -354,3 +365,49 @@ def test_pack_accepted_lookback_sizes(pkg, ctx, n):
         got = out.cpu()
         assert got[0].tolist() == [acc, n]
         assert torch.equal(got[1:1 + acc], exp[1:1 + acc])
+
+
+def test_pack_giveup_is_loud(pkg, ctx):
+    """A look-back that gives up must not pass silently: a forced
+    give-up of chunk 3 (and, separately, a spin limit of 1 over 1,221 chunks)
+    turns the header's accepted into -1, PointsExchange.check() raises, and the
+    next normal pack is exact again (the give-up counter was reset)."""
+    import importlib
+    import torch
+    par = importlib.import_module(pkg.__name__ + ".parallel")
+    n = 5_000_001
+    g = torch.Generator().manual_seed(3)
+    count = torch.randint(0, 8, (n,), generator=g, dtype=torch.int32)
+    mask = torch.randint(-2**62, 2**62, (n, 1), generator=g, dtype=torch.int64)
+    acc = int((count >= 3).sum())
+    dc, dm = count.cuda(), mask.cuda()
+    out = torch.full((acc + 2, 2), -9, dtype=torch.int64, device="cuda")
+    try:
+        ctx.pack_debug(-3)
+        torch.cuda.synchronize()
+        ctx.pack_accepted(0, dc, dm, 3, out)
+        torch.cuda.synchronize()
+        assert out[0].cpu().tolist() == [-1, n]
+        ex = par.PointsExchange(ctx, 1, acc + 1, torch.device("cuda:0"), points=False)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            b = ex.post(0, dc, dm, 3, stream=s)
+        with pytest.raises(RuntimeError, match="look-back gave up"):
+            ex.check(b)
+        # a spin limit of one iteration: whether a chunk gives up depends on
+        # the schedule; if one did, the header says so
+        ctx.pack_debug(1)
+        torch.cuda.synchronize()
+        ctx.pack_accepted(0, dc, dm, 3, out)
+        torch.cuda.synchronize()
+        h = out[0].cpu().tolist()
+        assert h == [-1, n] or h == [acc, n]
+    finally:
+        ctx.pack_debug(0)
+    torch.cuda.synchronize()
+    ctx.pack_accepted(0, dc, dm, 3, out)
+    torch.cuda.synchronize()
+    exp = torch.full((acc + 2, 2), -9, dtype=torch.int64)
+    par.pack_accepted_reference(0, count, mask, 3, exp)
+    got = out.cpu()
+    assert got[0].tolist() == [acc, n] and torch.equal(got[1:1 + acc], exp[1:1 + acc])

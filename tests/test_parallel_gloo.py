@@ -144,17 +144,13 @@ def _points_worker(rank, world, port, n, strong, sweeps, out_dir):
         _, mask, count, _ = sc.score_batch(c, ref, 0.4, 5)
         if ex is None:
             ex = par.PointsExchange(None, 1, n, torch.device("cpu"))
-        bi = ex.post(off, torch.from_numpy(count), torch.from_numpy(mask.view(np.int64)), 3)
-        idx, m = ex.result(bi)
-        # the records carry no geometry: a receiving rank regenerates the 3D
-        # point of any global index from the queue's definition
-        if strong:
-            whole = syn.candidates(n, K, R, t, seed=seed)[0]
-        else:
-            whole = np.concatenate([syn.candidates(n, K, R, t, seed=seed + r)[0] for r in range(world)])
-        out[f"idx{k}"], out[f"mask{k}"], out[f"pts{k}"] = idx.numpy(), m.numpy(), whole[idx.numpy()]
+        bi = ex.post(off, torch.from_numpy(count), torch.from_numpy(mask.view(np.int64)), 3,
+                     c=torch.from_numpy(np.ascontiguousarray(c)))
+        idx, m, pts = ex.result(bi)
+        # the rows carry the accepted 3D points themselves
+        out[f"idx{k}"], out[f"mask{k}"], out[f"pts{k}"] = idx.numpy(), m.numpy(), pts.numpy()
     # capacity overflow is reported, not silently truncated
-    small = par.PointsExchange(None, 1, 2, torch.device("cpu"))
+    small = par.PointsExchange(None, 1, 2, torch.device("cpu"), points=False)
     bi = small.post(0, torch.full((10,), 5, dtype=torch.int32), torch.ones((10, 1), dtype=torch.int64), 3)
     try:
         small.result(bi)
@@ -173,8 +169,8 @@ def test_accepted_points_exchange_gloo(tmp_path, orc, dino, world, n, strong):
     the ranks -- per-rank blocks (weak) or shard_range slices of one queue
     (strong) -- over three consecutive sweeps, and every rank ends each sweep
     with the whole sweep's accepted candidates (|V| >= 3) and masks in index
-    order (16-B records), as one process scoring the whole queue finds them,
-    and regenerates their 3D points from the global indices."""
+    order with their 3D points (40-B records), as one process scoring the
+    whole queue finds them."""
     import importlib
     syn = importlib.import_module(PKG_NAME + ".synthetic")
     sweeps = 3

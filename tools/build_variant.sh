@@ -6,4 +6,4 @@ D=$(cd "$(dirname "$0")/.." && pwd)/simple-implementation-of-structure-from-moti
 N=$1; shift
 cd $D/csrc && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared \
   -mllvm -amdgpu-atomic-optimizer-strategy=None -ffp-contract=off -fno-fast-math -Wno-unused-function "$@" \
-  -o $D/libmvs_amd_$N.so mvs_kernels.hip sfm_kernels.hip mvs_engine.cpp
+  -o $D/libmvs_amd_$N.so mvs_kernels.hip mvs_score_tab.hip sfm_kernels.hip mvs_engine.cpp

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 iteration: GPU tests (optionally -k $PYTEST_K), then the headline-only
+# bench with the tables scorer (k_score_tab) and the in-kernel-moments scorer
+# (MVS_SCORE_KERNEL=mma, k_score_mma) alternating on one box.
+export TMPDIR=/tmp
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+T=${TAG:-r4}
+if [ -z "$NO_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${T}_pytest.log 2>&1
+  rc=$?; tail -3 gpurun_out/${T}_pytest.log; [ $rc -ne 0 ] && { grep -B5 -A40 "FAILED\|Error\|error" gpurun_out/${T}_pytest.log | head -80; exit $rc; }
+fi
+B="--no-stage --no-ring --secondary-wid 0 --steps 100 --no-cpu-baseline ${BENCH_ARGS}"
+: > gpurun_out/${T}_ab.log
+for rep in 1 2; do
+  for v in tab mma; do
+    if [ $v = mma ]; then KM=mma; else KM=; fi
+    MVS_SCORE_KERNEL=$KM timeout -k 10 200 python bench.py $B > gpurun_out/${T}_b_$v.json 2>gpurun_out/${T}_b.err || { tail -5 gpurun_out/${T}_b.err; exit 1; }
+    python -c "
+import json,sys; d=json.loads(open('gpurun_out/${T}_b_$v.json').read().strip().splitlines()[-1])
+print('$v rep $rep: %.3f G cand/s  step %.1f us  kernel %.1f us (%s)  pack %.1f us' % (d['value']/1e9, d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, d['kernel'], d['exchange']['pack_us']))" | tee -a gpurun_out/${T}_ab.log
+  done
+done
