@@ -64,6 +64,29 @@ def logical_bytes(V, wid):
     return V * (2 * wid + 1) ** 2 + 32 + 8 * ((V + 63) // 64) + 16
 
 
+def score(cx, sw, wid, thr, stream):
+    """One sweep's photo test: records (mvs_score_device_rec, one 16-B store per
+    candidate at V <= 64) unless --soa asked for the three-array outputs."""
+    if sw["rec"] is not None:
+        cx.score_device_rec(sw["c"], sw["ref"], sw["xy"], sw["rec"], thr, wid, stream=stream.cuda_stream)
+    else:
+        cx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], thr, wid,
+                        stream=stream.cuda_stream)
+
+
+def pack_src(sw):
+    """(count, mask) arguments of the pack: (None, records) or the arrays."""
+    return (None, sw["rec"]) if sw["rec"] is not None else (sw["count"], sw["mask"])
+
+
+def host_outputs(sw, m=None):
+    """(mask uint64 (m, words), count int32 (m,)) of the last sweep, on the host."""
+    if sw["rec"] is not None:
+        r = sw["rec"][:m].cpu().numpy().view(np.uint64)[:, :-1]
+        return r, np.bitwise_count(r).sum(axis=1).astype(np.int32)
+    return sw["mask"][:m].cpu().numpy().view(np.uint64), sw["count"][:m].cpu().numpy()
+
+
 def load_scene():
     from PIL import Image
     import glob
@@ -79,14 +102,15 @@ def load_scene():
     return rgb, np.array(K), np.array(R), np.array(t)
 
 
-def pmc_entry(scene, V, wid, n):
-    """Per-launch counters of the scorer for this configuration from the
-    committed PMC profile, or None."""
+def pmc_entry(scene, V, wid, n, kernel):
+    """Per-launch counters of the scorer kernel `kernel` for this
+    configuration from the committed PMC profile, or None (counters of
+    another kernel never price this one)."""
     if not os.path.exists(PMC_PATH):
         return None
     try:
         for e in json.load(open(PMC_PATH))["entries"]:
-            if (e["scene"], e["V"], e["wid"], e["n"]) == (scene, V, wid, n):
+            if (e["scene"], e["V"], e["wid"], e["n"]) == (scene, V, wid, n) and kernel + "<" in e["kernel"]:
                 return e
     except Exception:
         return None
@@ -141,19 +165,19 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
     words = (V + 63) // 64
     row = 8 * par.points_width(words)
     cap = accepted + accepted // 16 + 256
-    out = torch.empty((cap + 1, par.points_width(words)), dtype=torch.int64, device=sw["count"].device)
+    out = torch.empty((cap + 1, par.points_width(words)), dtype=torch.int64, device=sw["c"].device)
+    pc, pm = pack_src(sw)
     for _ in range(3):
-        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream, c=sw["c"])
+        ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
     # device time: the packs queue up behind three sweeps' worth of scoring,
     # so the host's submission rate (a ctypes call + two launches per pack,
     # ~15 us) does not pace them
     for _ in range(3):
-        ctx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], thr, wid,
-                         stream=stream.cuda_stream)
+        score(ctx, sw, wid, thr, stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(20):
-        ctx.pack_accepted(sw["off"], sw["count"], sw["mask"], vlb, out, stream=stream.cuda_stream, c=sw["c"])
+        ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
     e1.record(stream)
     e1.synchronize()
     if int(out[0, 0].item()) != accepted:
@@ -165,6 +189,56 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
                     "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync), device time "
                     "of 20 packs queued behind scoring work; the "
                     "all-gather runs on its own stream behind the next sweep (parallel.PointsExchange)"}
+
+
+def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups=32):
+    """The N = 8 exchange's footprint beside scoring, on one GPU:
+    each step scores the sweep and packs its accepted rows (40 B) on the
+    scoring stream; a second stream waits for the pack and runs a copy kernel
+    of `workgroups` workgroups (RCCL's all-gather is a kernel on a few CUs)
+    moving the bytes one rank receives at N = 8, overlapping the next step.
+    Reported: the step alone, the step with the proxy, and the proxy alone."""
+    import torch
+    pkg = importlib.import_module(PKG_NAME)
+    par = importlib.import_module(PKG_NAME + ".parallel")
+    dev = sw["c"].device
+    pc, pm = pack_src(sw)
+    words = (V + 63) // 64
+    width = par.points_width(words)
+    cap = accepted + accepted // 16 + 256
+    recv = (7 * (cap + 1) * width * 8 + 15) // 16 * 16
+    src = torch.zeros(recv // 8, dtype=torch.int64, device=dev)
+    dst = torch.empty_like(src)
+    out = torch.empty((cap + 1, width), dtype=torch.int64, device=dev)
+    comm = torch.cuda.Stream(dev)
+
+    def run(k, with_proxy):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            score(ctx, sw, wid, thr, stream)
+            ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
+            if with_proxy:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                comm.wait_event(ev)
+                pkg._lib.proxy_copy(dst, src, recv, workgroups, comm.cuda_stream)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k
+
+    run(3, True)
+    alone = run(steps, False)
+    both = run(steps, True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(comm)
+    for _ in range(10):
+        pkg._lib.proxy_copy(dst, src, recv, workgroups, comm.cuda_stream)
+    e1.record(comm)
+    e1.synchronize()
+    return {"proxy": f"copy kernel of {workgroups} workgroups moving the N = 8 per-rank receive "
+                     f"({recv / 1e6:.1f} MB of 40-B rows) on a second stream after each step's pack",
+            "step_us_score_pack": alone * 1e6, "step_us_with_proxy": both * 1e6,
+            "proxy_alone_us": e0.elapsed_time(e1) / 10 * 1e3, "received_bytes": recv, "workgroups": workgroups}
 
 
 def main():
@@ -186,6 +260,9 @@ def main():
     ap.add_argument("--secondary-wid", type=int, default=3)
     ap.add_argument("--no-stage", action="store_true", help="skip the full-stage secondary")
     ap.add_argument("--no-ring", action="store_true", help="skip the ring256 secondary")
+    ap.add_argument("--no-overlap", action="store_true", help="skip the exchange overlap proxy")
+    ap.add_argument("--soa", action="store_true",
+                    help="score into the three output arrays (mask, count, avg) instead of one record per candidate")
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
                     help="headline scene (ring256: config 4 as the headline, for profiling)")
     a = ap.parse_args()
@@ -236,6 +313,7 @@ def main():
                 "xy": torch.empty((n, 2), dtype=torch.float64, device=dev),
                 "mask": torch.empty((n, (ctx_V + 63) // 64), dtype=torch.int64, device=dev),
                 "count": torch.empty(n, dtype=torch.int32, device=dev),
+                "rec": None if a.soa else torch.empty((n, (ctx_V + 63) // 64 + 1), dtype=torch.int64, device=dev),
                 "avg": torch.empty(n, dtype=torch.float64, device=dev)}
 
     def timed(cx, sw, wid, steps, warmup, exchange=True, rebuild=False):
@@ -248,14 +326,13 @@ def main():
                 evs[0].record(stream)
             if rebuild:
                 cx.rebuild(stream=stream.cuda_stream)
-            cx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], a.thr, wid,
-                            stream=stream.cuda_stream)
+            score(cx, sw, wid, a.thr, stream)
             if evs is not None:
                 evs[1].record(stream)
             if exchange and world > 1:
                 # pack (device, no host sync) + all-gather on the exchange's own
                 # stream, overlapping the next sweep (parallel.PointsExchange)
-                sw["exch"].post(sw["off"], sw["count"], sw["mask"], vlb, stream=stream, c=sw["c"])
+                sw["exch"].post(sw["off"], *pack_src(sw), vlb, stream=stream, c=sw["c"])
 
         for _ in range(warmup):
             step()
@@ -293,16 +370,16 @@ def main():
     if world > 1:
         # exchange capacity: this sweep's accepted count (one untimed score),
         # the maximum over ranks plus a margin (rows of every rank are equal-sized)
-        ctx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], a.thr, a.wid,
-                         stream=stream.cuda_stream)
-        kk = (sw["count"] >= vlb).sum().to(torch.int64).reshape(1)
+        score(ctx, sw, a.wid, a.thr, stream)
+        torch.cuda.synchronize()
+        kk = torch.tensor([int((host_outputs(sw)[1] >= vlb).sum())], dtype=torch.int64, device=dev)
         dist.all_reduce(kk, op=dist.ReduceOp.MAX)
         cap = int(kk.item()) + int(kk.item()) // 16 + 256
         sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap, dev)
     total_n = a.n if a.strong else a.n * world
     dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup)
     value = total_n * a.steps / dt
-    accepted = int((sw["count"] >= vlb).sum().item())
+    accepted = int((host_outputs(sw)[1] >= vlb).sum())
     kernel_name = ctx.timed_kernel()
     solo = rank == 0 and world == 1
 
@@ -328,6 +405,8 @@ def main():
                                f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
                                f"MIN_NCC {a.thr}, accepted points (index, view mask, x y z) all-gathered",
                    "global_batch": total_n, "wid": a.wid, "views": V,
+                   "outputs": ("per candidate: xy + mask, count, avg arrays" if a.soa else
+                               "per candidate: xy + one record [mask word, avg] (|V| = popcount)"),
                    "parallelism": f"candidate-queue shards x{world} (RCCL all-gather of accepted points)"},
         "kernel": kernel_name,
         "kernel_timing": f"HIP events around the scorer on every {TIME_EVERY}th timed step",
@@ -336,7 +415,10 @@ def main():
         "gathered_records": gathered,
         "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream, a.thr, a.wid),
     }
-    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n), V, a.wid, n, kms)
+    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms)
+    if solo and not a.no_overlap:
+        out["exchange"]["overlap_proxy"] = overlap_proxy(ctx, sw, V, vlb, accepted, stream, a.thr, a.wid,
+                                                         max(a.steps // 2, 10))
 
     if solo:
         # cold sweep: scene setup from the resident images + the sweep
@@ -351,7 +433,7 @@ def main():
             dt2, kms2, pms2, _ = timed(ctx, sw, a.secondary_wid, s2, 2, exchange=False)
             out["secondary"] = {"wid": a.secondary_wid, "value": n * s2 / dt2, "kernel_ms": kms2,
                                 "score_call_ms": pms2,
-                                "roofline": roofline(pmc_entry(a.scene, V, a.secondary_wid, n), V,
+                                "roofline": roofline(pmc_entry(a.scene, V, a.secondary_wid, n, kernel_name), V,
                                                      a.secondary_wid, n, kms2)}
 
     if solo and a.scene == "dino" and not a.no_stage:
@@ -388,8 +470,8 @@ def main():
                                       f"{rsw['n']} candidates per sweep, wid {a.wid}, MIN_NCC {a.thr}",
                           "value": rsw["n"] * s3 / rdt, "unit": "candidates/s", "kernel": rctx.timed_kernel(),
                           "kernel_ms": rkms, "score_call_ms": rpms,
-                          "accepted_per_sweep": int((rsw["count"] >= 3).sum().item()),
-                          "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"]), rV, a.wid,
+                          "accepted_per_sweep": int((host_outputs(rsw)[1] >= 3).sum()),
+                          "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"], rctx.timed_kernel()), rV, a.wid,
                                                rsw["n"], rkms)}
         rctx.close()
 
@@ -405,17 +487,16 @@ def main():
         scene.score_batch(sw["c_np"][:m], sw["ref_np"][:m], a.thr, a.wid, nthreads=ncores)
         cdt_all = time.perf_counter() - t0
         # the sample doubles as a parity spot check of the measured kernel
-        ctx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], a.thr, a.wid,
-                         stream=stream.cuda_stream)
+        score(ctx, sw, a.wid, a.thr, stream)
         torch.cuda.synchronize()
-        cnt_gpu = sw["count"][:m].cpu().numpy()
+        mask_gpu, cnt_gpu = host_outputs(sw, m)
         out["cpu_baseline"] = {
             "value": m / cdt, "unit": "candidates/s", "cores": 1, "kind": "port",
             "sample": f"first {m} of the rank-0 sweep (same candidates, wid={a.wid}), "
                       f"oracle/mvs_oracle.c or_score_batch single-threaded, {cdt:.1f} s",
             "value_all_cores": m / cdt_all, "cores_all": ncores,
             "parity_on_sample": bool(np.array_equal(cnt_gpu, ocount) and
-                                     np.array_equal(sw["mask"][:m].cpu().numpy().view(np.uint64), omask))}
+                                     np.array_equal(mask_gpu, omask))}
         # the reference itself (CPython, single thread): its recorded wall time
         # for the longest unfiltered fixture run and the photo tests that run
         # performed (tests/golden/gen_ref_timing.py)

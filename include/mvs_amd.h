@@ -81,6 +81,13 @@ int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int 
 int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
                      double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
                      double* d_avg, void* stream);
+/* The same photo test with one record per candidate instead of three arrays:
+ * d_rec[i * (words + 1) ...] = [mask words of i, avg_ncc_score as binary64
+ * bits]; |V| = the popcount of the mask words.  One 16-B store per candidate
+ * at V <= 64 (the scorer's output stores are scattered by candidate id).
+ * d_rec 16-B aligned; mvs_pack_accepted reads it with d_count = NULL. */
+int mvs_score_device_rec(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
+                         double min_ncc, double* d_xy, int64_t* d_rec, void* stream);
 /* CellTable.filter_out_outlier (MVS2.py:132-158) on the host, over n accepted
  * patches in fill order (what the stage's opt-in filter mode runs between
  * the expansion and reconstruct_from_Q): patch e has cell[2e..2e+1] =
@@ -101,6 +108,8 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
  * [offset + i, mask words of i, and with d_c (the slice's n*3 centres, the
  * candidates' 3D points) the binary64 bits of x, y, z] (40 B at V <= 64;
  * d_c = NULL: 16 B, the receiver regenerating a point from its global index).
+ * d_count = NULL: d_mask is mvs_score_device_rec's records (words + 1 int64
+ * each) and |V| their popcount.
  * Device pointers, stream-ordered, no host synchronisation (the accepted
  * total is in the header; a slice with more than cap accepted keeps its
  * first cap).  accepted = -1 in the header means the pack's look-back gave
@@ -109,6 +118,11 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
 int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count,
                       const uint64_t* d_mask, const double* d_c, int vlb, int64_t cap, int64_t* d_out,
                       void* stream);
+/* Measurement only (bench.py exchange.overlap_proxy): copies bytes (a
+ * multiple of 16) from d_src to d_dst with a kernel of `workgroups`
+ * 256-thread workgroups on `stream` -- the CU footprint of a collective's
+ * kernel, run beside the scoring kernels on one GPU. */
+int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups, void* stream);
 /* Tests only: mode > 0 sets the pack's look-back spin limit, mode < 0 makes
  * chunk -mode (4096 candidates each) give up at once, 0 restores the default. */
 int mvs_pack_debug(mvs_ctx* ctx, int64_t mode);

@@ -33,9 +33,12 @@ SIGNATURES = [
                                  _dp, _u64p, _i32p, _dp]),
     ("mvs_score_device", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int,
                                         ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
+    ("mvs_score_device_rec", ctypes.c_int, [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, ctypes.c_double,
+                                            _vp, _vp, _vp]),
     ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
                                          ctypes.c_int64, _vp, _vp]),
     ("mvs_pack_debug", ctypes.c_int, [_vp, ctypes.c_int64]),
+    ("mvs_proxy_copy", ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp]),
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
                                            _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
     ("mvs_exact_hits", ctypes.c_int64, [_vp]),
@@ -309,21 +312,35 @@ class MvsContext:
                                      stream if stream is not None else None)
         check(rc, self._h, "mvs_score_device")
 
+    def score_device_rec(self, c, ref, xy, rec, min_ncc=0.7, wid=5, stream=None):
+        """The photo test into records (device int64 tensor (n, words + 1): mask
+        words, avg bits; |V| = popcount), stream-ordered."""
+        n = int(ref.numel())
+        if rec.dtype.itemsize != 8 or tuple(rec.shape) != (n, self.words + 1) or not rec.is_contiguous():
+            raise RuntimeError(f"score_device_rec: rec must be contiguous int64 ({n}, {self.words + 1})")
+        rc = load().mvs_score_device_rec(self._h, n, c.data_ptr(), ref.data_ptr(), int(wid), float(min_ncc),
+                                         xy.data_ptr(), rec.data_ptr(), stream if stream is not None else None)
+        check(rc, self._h, "mvs_score_device_rec")
+
     def pack_accepted(self, offset, count, mask, vlb, out, stream=None, c=None):
         """mvs_pack_accepted: the accepted candidates (count >= vlb) of a scored
         slice as exchange rows of out (device int64 tensor (cap + 1, width):
         row 0 = [accepted, n, 0...] (accepted = -1: the pack failed), then
         [offset + i, mask words(, x y z bits with c)] in index order); c = the
         slice's (n, 3) float64 centres or None (width 1 + words [+ 3]);
-        stream-ordered, no host sync."""
-        n = int(count.numel())
+        stream-ordered, no host sync.  count None: mask is score_device_rec's
+        records and |V| their popcount."""
+        n = int(count.numel()) if count is not None else int(mask.shape[0])
+        if count is None and (mask.dtype.itemsize != 8 or mask.shape[1] != self.words + 1):
+            raise RuntimeError("pack_accepted: records must be int64 (n, words + 1)")
         cap = int(out.shape[0]) - 1
         width = 1 + self.words + (3 if c is not None else 0)
         if out.dtype.itemsize != 8 or out.shape[1] != width or not out.is_contiguous():
             raise RuntimeError(f"pack_accepted: out must be contiguous int64 (cap + 1, {width})")
         if c is not None and (c.dtype.itemsize != 8 or tuple(c.shape) != (n, 3) or not c.is_contiguous()):
             raise RuntimeError("pack_accepted: c must be contiguous float64 (n, 3)")
-        rc = load().mvs_pack_accepted(self._h, n, int(offset), count.data_ptr(), mask.data_ptr(),
+        rc = load().mvs_pack_accepted(self._h, n, int(offset), count.data_ptr() if count is not None else None,
+                                      mask.data_ptr(),
                                       c.data_ptr() if c is not None else None,
                                       int(vlb), cap, out.data_ptr(),
                                       stream if stream is not None else None)
@@ -509,6 +526,13 @@ class Stage:
             self.close()
         except Exception:
             pass
+
+
+def proxy_copy(dst, src, nbytes, workgroups, stream=None):
+    """Measurement only: copy nbytes between device tensors with a kernel of
+    `workgroups` workgroups on `stream` (a collective's CU footprint)."""
+    check(load().mvs_proxy_copy(dst.data_ptr(), src.data_ptr(), int(nbytes), int(workgroups), stream),
+          None, "mvs_proxy_copy")
 
 
 def ncc_windows(a, b, thr, force_exact=False, stream=None):

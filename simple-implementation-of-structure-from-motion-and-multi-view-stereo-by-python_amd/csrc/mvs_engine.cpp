@@ -456,6 +456,8 @@ int guarded(mvs_ctx* ctx, Fn&& fn) {
     }
 }
 
+// d_count == null: d_mask holds records [mask words, avg bits] of words + 1
+// int64 each (mvs_score_device_rec), d_avg is ignored
 void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
                   double thr, double* d_xy, uint64_t* d_mask, int32_t* d_count, double* d_avg,
                   hipStream_t s) {
@@ -470,6 +472,14 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
     a.count = d_count;
     a.avg = d_avg;
     a.exact_hits = ctx->d_exact.p;
+    a.mstride = ctx->words();
+    a.astride = 1;
+    a.rec = 0;
+    if (!d_count) {
+        a.rec = 1;
+        a.mstride = a.astride = ctx->words() + 1;
+        a.avg = (double*)(d_mask + ctx->words());
+    }
     // the tiled matrix-core scorer (k_score_mma, any V <= 256) for batches of
     // >= 2048 candidates; the direct k_score for small batches
     const bool grouped = ctx->V > MVS_GROUP_VIEWS;
@@ -1421,9 +1431,23 @@ int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* 
                      double* d_avg, void* stream) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
     if (n < 0) return set_err(ctx, Fail{MVS_E_ARG, "n < 0"});
+    if (n > 0 && (!d_c || !d_ref || !d_xy || !d_mask || !d_count))
+        return set_err(ctx, Fail{MVS_E_ARG, "null device pointer"});
     return guarded(ctx, [&]() {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         score_device(ctx, n, d_c, d_ref, wid, min_ncc, d_xy, d_mask, d_count, d_avg, s);
+        return 0;
+    });
+}
+
+int mvs_score_device_rec(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
+                         double min_ncc, double* d_xy, int64_t* d_rec, void* stream) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (n < 0 || (n > 0 && (!d_c || !d_ref || !d_xy || !d_rec)) || ((uintptr_t)d_rec & 15) != 0)
+        return set_err(ctx, Fail{MVS_E_ARG, "bad arguments (records must be 16-B aligned)"});
+    return guarded(ctx, [&]() {
+        hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+        score_device(ctx, n, d_c, d_ref, wid, min_ncc, d_xy, (uint64_t*)d_rec, nullptr, nullptr, s);
         return 0;
     });
 }
@@ -1443,7 +1467,7 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
 int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count, const uint64_t* d_mask,
                       const double* d_c, int vlb, int64_t cap, int64_t* d_out, void* stream) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
-    if (n < 0 || cap < 0 || !d_out || (n > 0 && (!d_count || !d_mask)))
+    if (n < 0 || cap < 0 || !d_out || (n > 0 && !d_mask))
         return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
     return guarded(ctx, [&]() {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
@@ -1470,6 +1494,14 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
         ctx->scratch_release(s);
         return 0;
     });
+}
+
+int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups, void* stream) {
+    if (bytes < 0 || (bytes % 16) != 0 || workgroups < 1 || (bytes > 0 && (!d_dst || !d_src)))
+        return set_err(nullptr, Fail{MVS_E_ARG, "bad arguments"});
+    if (mvs_launch_proxy_copy(d_dst, d_src, bytes, workgroups, (hipStream_t)stream) != 0)
+        return set_err(nullptr, Fail{MVS_E_HIP, "proxy copy launch failed"});
+    return 0;
 }
 
 int mvs_pack_debug(mvs_ctx* ctx, int64_t mode) {

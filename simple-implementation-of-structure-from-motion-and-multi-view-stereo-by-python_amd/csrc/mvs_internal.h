@@ -49,10 +49,13 @@ struct ScoreArgs {
     const int32_t* ref;   // n
     double thr;
     double* xy;           // n*2 (projection into ref view, MVS2.py:63)
-    uint64_t* mask;       // n*words
-    int32_t* count;       // n
-    double* avg;          // n (may be null)
+    uint64_t* mask;       // candidate i's words at mask[i * mstride]
+    int32_t* count;       // n (null: records, |V| = popcount of the mask)
+    double* avg;          // avg[i * astride] (may be null)
     int32_t* exact_hits;  // 1 counter: lanes that took the exact (numpy-order) path
+    int64_t mstride;      // words (separate arrays) or words + 1 (records)
+    int64_t astride;      // 1 (separate arrays) or words + 1 (records)
+    int rec;              // 1: records [mask words, avg bits] of words + 1 int64 each
 };
 
 // Scratch of the tiled scorer (device pointers, sized by the host).
@@ -185,6 +188,8 @@ int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hip
 int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, const double* c,
                              int words, int vlb, int64_t cap, uint64_t* status, uint64_t* aux, uint64_t epoch,
                              int32_t* err, int64_t debug, int64_t* out, hipStream_t s);
+// measurement only: a copy of bytes (multiple of 16) by `workgroups` workgroups
+int mvs_launch_proxy_copy(void* dst, const void* src, int64_t bytes, int workgroups, hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,
                            int force_exact, double* ncc, uint8_t* pass, hipStream_t s);
 // stage output order on the device (reconstruct_from_Q, MVS2.py:159-173):

@@ -180,14 +180,14 @@ DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fe
     }
     if (!avg_out || cnt == 0) {
         if (lane == 0) {
-            *count_out = cnt;
+            if (count_out) *count_out = cnt;
             if (avg_out) *avg_out = 0.0;
         }
         return;
     }
     const double tot = wave_sum(acc);
     if (lane == 0) {
-        *count_out = cnt;
+        if (count_out) *count_out = cnt;
         *avg_out = tot / cnt;
     }
 }
@@ -210,7 +210,7 @@ DEV void wave_score_empty(uint64_t* mask_out, int32_t* count_out, double* avg_ou
     const int lane = threadIdx.x & 63;
     if (lane < NS && lane < words) mask_out[lane] = 0;
     if (lane == 0) {
-        *count_out = 0;
+        if (count_out) *count_out = 0;
         if (avg_out) *avg_out = 0.0;
     }
 }
@@ -291,13 +291,14 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
     if (lane == 0) { a.xy[2 * cand] = px; a.xy[2 * cand + 1] = py; }
     int q, r;
     if (!window_ok(sc, px, py, WID, &q, &r)) {
-        wave_score_empty<NS>(a.mask + cand * words, a.count + cand, a.avg ? a.avg + cand : nullptr, words);
+        wave_score_empty<NS>(a.mask + cand * a.mstride, a.count ? a.count + cand : nullptr,
+                             a.avg ? a.avg + cand * a.astride : nullptr, words);
         return;
     }
     q = __builtin_amdgcn_readfirstlane(q);
     r = __builtin_amdgcn_readfirstlane(r);
-    wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * words, a.count + cand,
-                        a.avg ? a.avg + cand : nullptr, a.exact_hits);
+    wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * a.mstride, a.count ? a.count + cand : nullptr,
+                        a.avg ? a.avg + cand * a.astride : nullptr, a.exact_hits);
 }
 
 // ---------------------------------------------------------------------------
@@ -384,9 +385,9 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         a.xy[2 * i + 1] = py;
         int q, r;
         if (!window_ok(sc, px, py, wid, &q, &r)) {
-            for (int w = 0; w < words; ++w) a.mask[i * words + w] = 0;
-            a.count[i] = 0;
-            if (a.avg) a.avg[i] = 0.0;
+            for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
+            if (a.count) a.count[i] = 0;
+            if (a.avg) a.avg[i * a.astride] = 0.0;
             continue;
         }
         const int tx = q / MVS_TILE_W, ty = r / MVS_TILE_H;
@@ -1096,8 +1097,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     #else
                         {
     #endif
-                        a.mask[idx] = mk;
-                        a.count[idx] = cnt;
+                        a.mask[idx * a.mstride] = mk;
+                        if (a.count) a.count[idx] = cnt;
                         }
                         if (a.avg && MVS_DIAG_STORE_OK(idx)) {
                             // its own term num_RR w_a = D_a w_a = sqrt(D_a) = 1 / w_a (to
@@ -1105,7 +1106,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                             double inv = __builtin_amdgcn_rcp(my_wa[h]);
                             inv = inv * (2.0 - my_wa[h] * inv);
                             const double sum = self ? mine - inv : mine;
-                            a.avg[idx] = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
+                            a.avg[idx * a.astride] = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
                         }
                         if (gg) {
                             t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
@@ -1536,7 +1537,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             prefetch();
             // the previous group's mask word: its store has phases 3-4 to complete
             // (the barrier after phase 4 waits for it with the region's LDS-DMA)
-            if (g > 0 && tid < nc) a.mask[(int64_t)my_idx * words + g - 1] = pend;
+            if (g > 0 && tid < nc) a.mask[(int64_t)my_idx * a.mstride + g - 1] = pend;
             asm volatile("" ::: "memory");   // the LDS-DMA issues stay ahead of phase 3
             STAMP(tpf);
 
@@ -1699,9 +1700,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             kpar ^= 1;
         }
         if (tid < nc) {
-            a.mask[(int64_t)my_idx * words + NG - 1] = pend;
-            a.count[my_idx] = acnt;
-            if (a.avg) a.avg[my_idx] = acnt ? asum * (1.0 / (double)acnt) : 0.0;
+            a.mask[(int64_t)my_idx * a.mstride + NG - 1] = pend;
+            if (a.count) a.count[my_idx] = acnt;
+            if (a.avg) a.avg[(int64_t)my_idx * a.astride] = acnt ? asum * (1.0 / (double)acnt) : 0.0;
             if (aguard) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4(my_idx, tile, cand[tid].y, 0);
         }
         if (next >= n_items) break;
@@ -1729,8 +1730,8 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
         const int pk = __builtin_amdgcn_readfirstlane(f.z);
         const int ty = tile / t.ntx, tx = tile - ty * t.ntx;
         const int q = tx * MVS_TILE_W + (pk & 15), r = ty * MVS_TILE_H + ((pk >> 4) & 7), R = pk >> 7;
-        wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * words, a.count + cand,
-                            a.avg ? a.avg + cand : nullptr, a.exact_hits);
+        wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * a.mstride, a.count ? a.count + cand : nullptr,
+                            a.avg ? a.avg + cand * a.astride : nullptr, a.exact_hits);
     }
     __syncthreads();
     if (threadIdx.x == 0 && atomicAdd(t.done, 1) == (int)gridDim.x - 1) {
@@ -1980,6 +1981,8 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
     __shared__ int64_t s_base;                        // -1: no valid prefix (this chunk writes no rows)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int width = 1 + words + (cpt ? 3 : 0);
+    // count == null: the scorer's records [mask words, avg], |V| = popcount
+    const int64_t ms = count ? words : words + 1;
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     const int64_t nch = nchunk > 0 ? nchunk : 1;      // an empty slice still has chunk 0
     const uint64_t E = epoch << 34;
@@ -1991,7 +1994,15 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            c[j] = i < n ? count[i] : 0;
+            int cc = 0;
+            if (i < n) {
+                if (count) {
+                    cc = count[i];
+                } else {
+                    for (int q = 0; q < words; ++q) cc += __popcll(mask[i * ms + q]);
+                }
+            }
+            c[j] = cc;
         }
         uint64_t m[kAccPer], w0[kAccPer];
 #pragma unroll
@@ -1999,7 +2010,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
             const bool acc = i < n && c[j] >= vlb;
             m[j] = __ballot(acc);
-            w0[j] = acc ? mask[i * words] : 0ull;
+            w0[j] = acc ? mask[i * ms] : 0ull;
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
         }
         __syncthreads();
@@ -2083,7 +2094,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                         int64_t* o = out + (1 + pos) * width;
                         o[0] = offset + i;
                         o[1] = (int64_t)w0[j];
-                        for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * words + q];
+                        for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
                         if (cpt) {
                             // the accepted 3D point itself (binary64 bits)
                             o[1 + words] = __double_as_longlong(cpt[3 * i]);
@@ -2108,6 +2119,13 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
         }
         __syncthreads();
     }
+}
+
+// Measurement only (bench.py exchange.overlap_proxy): a copy of n 16-B pieces
+// by a fixed number of workgroups -- the footprint of an RCCL all-gather's
+// kernel (a few CUs streaming bytes) -- to run beside the scoring kernels.
+__global__ __launch_bounds__(256) void k_proxy_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
 }
 
 // reconstruct_from_Q (MVS2.py:159-173): an accepted patch is appended under
@@ -2420,6 +2438,13 @@ extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t
     // n == 0 still writes the header (chunk 0 of an empty slice)
     hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, c, words, vlb, cap,
                        status, aux, epoch, err, debug, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int mvs_launch_proxy_copy(void* dst, const void* src, int64_t bytes, int workgroups, hipStream_t s) {
+    if (bytes <= 0) return 0;
+    hipLaunchKernelGGL(k_proxy_copy, dim3(std::max(workgroups, 1)), dim3(256), 0, s, (const uint4*)src, (uint4*)dst,
+                       bytes / 16);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

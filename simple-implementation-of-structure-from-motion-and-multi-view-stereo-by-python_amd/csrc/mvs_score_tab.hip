@@ -521,14 +521,23 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                         mk &= ~(1ull << Rv[h]);
                         const int cnt = __popcll(mk);
                         const int64_t idx = e[h].x;
-                        a.mask[idx] = mk;
-                        a.count[idx] = cnt;
+                        double av = 0.0;
                         if (a.avg) {
                             // its own term num_RR w_a = D_a w_a = 1 / w_a leaves the sum
                             double inv = __builtin_amdgcn_rcp(my_wa[h]);
                             inv = inv * (2.0 - my_wa[h] * inv);
                             const double sum = self ? mine - inv : mine;
-                            a.avg[idx] = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
+                            av = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
+                        }
+                        if (a.rec) {
+                            // one 16-B record [mask word, avg] (|V| = popcount)
+                            const unsigned long long ab = __double_as_longlong(av);
+                            *(uint4*)(a.mask + 2 * idx) = make_uint4((uint32_t)mk, (uint32_t)(mk >> 32), (uint32_t)ab,
+                                                                     (uint32_t)(ab >> 32));
+                        } else {
+                            a.mask[idx] = mk;
+                            a.count[idx] = cnt;
+                            if (a.avg) a.avg[idx] = av;
                         }
                         if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
                     }

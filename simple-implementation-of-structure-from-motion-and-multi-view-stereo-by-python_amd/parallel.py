@@ -20,6 +20,7 @@ no communication while scoring.  Two exchanges:
   (8 B per child at V <= 64) are all-gathered; every rank then runs the
   identical ordered commit (mvs_stage_* in include/mvs_amd.h).
 """
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -42,9 +43,13 @@ def pack_accepted_reference(offset, count, mask, vlb, out, c=None):
     gloo process groups of the CPU tests): header [accepted, n, 0...], then
     up to cap rows in index order (with c: the points' bits after the mask
     words).  Device tensors never come here."""
-    if count.is_cuda:
+    if mask.is_cuda:
         raise RuntimeError("pack_accepted_reference is for CPU tensors; device slices use mvs_pack_accepted")
     cap = out.shape[0] - 1
+    if count is None:        # records [mask words, avg bits]: |V| = popcount
+        mask = mask[:, :-1]
+        count = torch.from_numpy(np.bitwise_count(mask.contiguous().numpy().view(np.uint64)).sum(axis=1)
+                                 .astype(np.int32))
     words = mask.shape[1]
     idx = torch.nonzero(count >= vlb).squeeze(1)
     out.zero_()
@@ -97,7 +102,7 @@ class PointsExchange:
         cc = c if self.points else None
         b = self.posted & 1
         self.posted += 1
-        if count.is_cuda:
+        if mask.is_cuda:
             cur = stream if stream is not None else torch.cuda.current_stream(self.device)
             if cur.cuda_stream == 0:
                 # the C-ABI reads stream 0 as "the library's own stream": the pack

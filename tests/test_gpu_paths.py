@@ -411,3 +411,51 @@ def test_pack_giveup_is_loud(pkg, ctx):
     par.pack_accepted_reference(0, count, mask, 3, exp)
     got = out.cpu()
     assert got[0].tolist() == [acc, n] and torch.equal(got[1:1 + acc], exp[1:1 + acc])
+
+
+def test_score_records_vs_arrays_and_pack(pkg, ctx, dino, orc):
+    """mvs_score_device_rec (one [mask, avg] record per candidate, |V| by
+    popcount) gives the three-array outputs bit for bit -- tiled scorer (the
+    bench's 2^20 sweep, and the oracle on its first 20k candidates) and direct
+    path (a small batch) -- and the pack reads the records (d_count NULL) into
+    the same exchange rows as from the arrays."""
+    import importlib
+    import torch
+    par = importlib.import_module(pkg.__name__ + ".parallel")
+    rgb, K, R, t = dino
+    dev = torch.device("cuda:0")
+    for n in (1 << 20, 1500):
+        c, ref = bench_candidates(n, K, R, t, seed=11)
+        tc, tr = torch.from_numpy(c).to(dev), torch.from_numpy(ref).to(dev)
+        xy = torch.empty((n, 2), dtype=torch.float64, device=dev)
+        mask = torch.empty((n, 1), dtype=torch.int64, device=dev)
+        count = torch.empty(n, dtype=torch.int32, device=dev)
+        avg = torch.empty(n, dtype=torch.float64, device=dev)
+        rec = torch.full((n, 2), -5, dtype=torch.int64, device=dev)
+        xy2 = torch.empty_like(xy)
+        torch.cuda.synchronize()
+        ctx.score_device(tc, tr, xy, mask, count, avg, 0.7, 5)
+        torch.cuda.synchronize()
+        ctx.score_device_rec(tc, tr, xy2, rec, 0.7, 5)
+        torch.cuda.synchronize()
+        r = rec.cpu().numpy()
+        m = mask.cpu().numpy()
+        assert np.array_equal(r[:, 0], m[:, 0]) and np.array_equal(xy.cpu().numpy(), xy2.cpu().numpy())
+        assert np.array_equal(np.bitwise_count(r[:, 0].view(np.uint64)).astype(np.int32), count.cpu().numpy())
+        assert np.array_equal(r[:, 1].view(np.float64), avg.cpu().numpy())
+        k = min(n, 20000)
+        oxy, omask, ocount, oavg = orc.Scene(rgb, K, R, t).score_batch(c[:k], ref[:k], 0.7, 5, nthreads=8)
+        assert np.array_equal(r[:k, 0].view(np.uint64), omask[:, 0])
+        assert np.allclose(r[:k, 1].view(np.float64), oavg, rtol=0, atol=AVG_TOL)
+        acc = int((count >= 3).sum())
+        w = par.points_width(1)
+        o1 = torch.full((acc + 5, w), -9, dtype=torch.int64, device=dev)
+        o2 = torch.full((acc + 5, w), -9, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        ctx.pack_accepted(3, count, mask, 3, o1, c=tc)
+        ctx.pack_accepted(3, None, rec, 3, o2, c=tc)
+        torch.cuda.synchronize()
+        assert int(o1[0, 0]) == acc and torch.equal(o1, o2)
+        exp = torch.full((acc + 5, w), -9, dtype=torch.int64)
+        par.pack_accepted_reference(3, None, rec.cpu(), 3, exp, torch.from_numpy(c))
+        assert torch.equal(o2.cpu()[:1 + acc], exp[:1 + acc])

@@ -1,5 +1,5 @@
-"""Merge rocprofv3 --pmc pass directories into a pmc.json (profiles/r03/): the
-per-launch counters of the scorer kernel (k_score_mma*) for one bench
+"""Merge rocprofv3 --pmc pass directories into a pmc.json (profiles/rNN/): the
+per-launch counters of the scorer kernel (k_score_tab / k_score_mma*) for one bench
 configuration.  bench.py reads this file to compute its roofline fractions.
 usage: pmc_json.py OUT.json SCENE V WID N PMC_DIR"""
 import collections
@@ -14,7 +14,7 @@ acc = collections.defaultdict(lambda: collections.defaultdict(lambda: collection
 for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
         acc[row["Kernel_Name"]][row["Counter_Name"]][(f, row["Dispatch_Id"])] += float(row["Counter_Value"])
-hits = [k for k in acc if "k_score_mma" in k]
+hits = [k for k in acc if "k_score_mma" in k or "k_score_tab" in k]
 if len(hits) != 1:
     sys.exit(f"scorer kernel ambiguous: {hits}")
 k = hits[0]
