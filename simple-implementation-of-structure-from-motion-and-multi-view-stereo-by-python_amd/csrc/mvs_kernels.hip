@@ -1716,14 +1716,22 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
 // a batch: it leaves the counters zero for the next one (the tile counts by
 // a grid-stride pass; the list's count, the item count and the queue head by
 // the workgroup that finishes last, after every workgroup has read them).
+// The grid has kFixBase workgroups plus, for large batches, more that take
+// part only when the list is long (a skewed batch whose tiles overflow their
+// buckets): a guard-band list of a few hundred entries costs no extra
+// workgroups' atomics, a long overflow list gets up to 4x the workgroups.
+constexpr int kFixBase = 64, kFixSmall = kFixBase * 4 * 8;
+
 template <int WID, int NS>
 __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t) {
     const int nfix = *t.fix_count;
+    const int active = nfix > kFixSmall ? (int)gridDim.x : kFixBase;   // uniform over the grid
+    if ((int)blockIdx.x >= active) return;
     const int words = (sc.V + 63) >> 6;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += gridDim.x * 256) t.tile_count[k] = 0;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += active * 256) t.tile_count[k] = 0;
     for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
-         k += gridDim.x * 4) {
+         k += active * 4) {
         const int4 f = t.fix_list[k];
         const int64_t cand = __builtin_amdgcn_readfirstlane(f.x);
         const int tile = __builtin_amdgcn_readfirstlane(f.y);
@@ -1734,7 +1742,7 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
                             a.avg ? a.avg + cand * a.astride : nullptr, a.exact_hits);
     }
     __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(t.done, 1) == (int)gridDim.x - 1) {
+    if (threadIdx.x == 0 && atomicAdd(t.done, 1) == active - 1) {
         *t.fix_count = 0;
         *t.n_items = 0;
         t.tile_count[t.ntiles] = 0;   // the queue head
@@ -2310,7 +2318,9 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         }
     }
     if (rc) return rc;
-    constexpr int kFixBlocks = 64;   // 256 waves, one guard-band candidate each at a time
+    // 256 waves (one candidate each at a time) for the guard band; up to 4x as
+    // many for a batch whose overflow list is long
+    const int kFixBlocks = (int)std::min<int64_t>(std::max<int64_t>(a->n / 4096, kFixBase), 4 * kFixBase);
     if (grouped) {
         if (sc->V <= 128)
             hipLaunchKernelGGL((k_score_fix<WID, 2>), dim3(kFixBlocks), dim3(256), 0, s, *sc, *a, *t);

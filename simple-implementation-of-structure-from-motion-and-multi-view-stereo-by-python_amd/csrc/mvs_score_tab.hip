@@ -129,6 +129,20 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
 // The other workgroup on the CU fills the issue slots this one leaves at its
 // barrier and in its latency waits.
 // ---------------------------------------------------------------------------
+#ifdef MVS_STAMPS
+// diagnostic build only: per-workgroup cycle sums (lane 0 of every wave adds
+// its own): slot 0 rounds (wave 0), 1 barrier wait at the round's start, 2
+// the wave's sort, 3 its units, 4 its M-blocks, 5 K-loops, 6 epilogues;
+// read by mvs_read_stamps_tab
+__device__ unsigned long long g_stamps_tab[1024 * 16];
+#define TSTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define TSTAMP_ADD(slot, val) \
+    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps_tab[(blockIdx.x & 1023) * 16 + (slot)], (unsigned long long)(val)); } while (0)
+#else
+#define TSTAMP(var)
+#define TSTAMP_ADD(slot, val)
+#endif
+
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = 512;
 constexpr int kTabChunk = MVS_MMA_CHUNK;
 
@@ -243,8 +257,10 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
         int2* cand = (int2*)cand_buf(bufc);
         const int zoff = RB;   // the zero row, relative to the region buffer
         // ---- 1. this item's region and list have landed (every wave's DMA) ----
+        TSTAMP(ts0);
         if (tid == 0) s_ids[0] = pend;
         __syncthreads();
+        TSTAMP(ts1);
         const int nx2 = __builtin_amdgcn_readfirstlane(s_ids[0]);
         // the next item's region and list into the other buffer, the descriptor
         // after it, thread 0's claim of the one after that
@@ -281,6 +297,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
+        TSTAMP(ts2);
         // ---- 3. + 4. units of two M-blocks (32 consecutive sorted candidates) ----
         for (int fb = b0; fb < b1; fb += 2) {
             const int nh = min(2, b1 - fb);
@@ -334,6 +351,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                         }
                     }
                 };
+                TSTAMP(tk0);
                 // the unit's candidates are sorted by row pair: its window rows lie
                 // in candidate 0's pair to the last valid candidate's pair + NB - 1
                 const int last = min(16 * NH - 1, nc - 1 - fb * 16);
@@ -419,6 +437,8 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                         kpass(std::integral_constant<int, KSK>{}, std::integral_constant<int, KSK>{}, I{},
                               min(sd, KS - KSK), sd);
                 }
+                TSTAMP(tk1);
+                TSTAMP_ADD(5, tk1 - tk0);
                 // the first candidate step's table values (issued after the K-loop:
                 // in flight across it they would hold 18 registers)
                 fetch(std::integral_constant<int, 0>{});
@@ -542,10 +562,18 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                         if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
                     }
                 }
+                TSTAMP(tk2);
+                TSTAMP_ADD(6, tk2 - tk1);
             };
             if (nh == 2) unit(std::integral_constant<int, 2>{});
             else unit(std::integral_constant<int, 1>{});
+            TSTAMP_ADD(4, nh);
         }
+        TSTAMP(ts3);
+        if (wave == 0) TSTAMP_ADD(0, 1);
+        TSTAMP_ADD(1, ts1 - ts0);
+        TSTAMP_ADD(2, ts2 - ts1);
+        TSTAMP_ADD(3, ts3 - ts2);
         if (nx1 >= n_units) return false;
         if constexpr (!DB) {
             // one buffer: every wave is done with it before the next item lands
@@ -587,6 +615,12 @@ int launch_tab_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, con
 }
 
 }  // namespace
+
+#ifdef MVS_STAMPS
+extern "C" int mvs_read_stamps_tab(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_tab), sizeof(g_stamps_tab)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int mvs_launch_moments(const SceneDev* sc, const MomentsDev* mt, hipStream_t s) {
     if (sc->V > 64 || mt->VP != 16 * ((sc->V + 15) / 16)) return -3;

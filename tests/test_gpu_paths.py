@@ -268,7 +268,7 @@ def test_timed_kernel_name(ctx, dino):
     ctx.score(c, ref, 0.7, 5)
     ms, k = ctx.kernel_time()
     ctx.kernel_timing(False)
-    assert k == 1 and ms > 0 and ctx.timed_kernel() == "k_score_mma"
+    assert k == 1 and ms > 0 and ctx.timed_kernel() == "k_score_tab"
 
 
 def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
@@ -459,3 +459,72 @@ def test_score_records_vs_arrays_and_pack(pkg, ctx, dino, orc):
         exp = torch.full((acc + 5, w), -9, dtype=torch.int64)
         par.pack_accepted_reference(3, None, rec.cpu(), 3, exp, torch.from_numpy(c))
         assert torch.equal(o2.cpu()[:1 + acc], exp[:1 + acc])
+
+
+def test_skewed_batch_overflow_cost(pkg, ctx, dino, orc):
+    """A skewed sweep: 2^18 candidates crowded onto two pixel tiles,
+    so that most of them overflow the tile buckets (cap = 16x the mean load)
+    into the direct path's list.  Outputs stay exact (a 4,000-candidate sample
+    against the oracle) and the whole call stays bounded: the direct path's
+    grid grows with the batch (up to 256 workgroups)."""
+    import time
+    import torch
+    rgb, K, R, t = dino
+    rng = np.random.default_rng(13)
+    n = 1 << 18
+    ref = rng.integers(0, 48, n).astype(np.int32)
+    x = np.where(rng.random(n) < 0.5, 300.0, 333.0) + rng.random(n) * 15.9
+    y = 200 + rng.random(n) * 7.9
+    z = rng.uniform(0.6, 0.72, n)
+    Kinv = np.linalg.inv(K)
+    ray = np.einsum("nij,nj->ni", Kinv[ref], np.stack([x, y, np.ones(n)], 1))
+    c = np.einsum("nji,nj->ni", R[ref], z[:, None] * ray - t[ref].reshape(n, 3))
+    dev = torch.device("cuda:0")
+    tc, tr = torch.from_numpy(np.ascontiguousarray(c)).to(dev), torch.from_numpy(ref).to(dev)
+    xy = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    mask = torch.empty((n, 1), dtype=torch.int64, device=dev)
+    count = torch.empty(n, dtype=torch.int32, device=dev)
+    avg = torch.empty(n, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    ctx.score_device(tc, tr, xy, mask, count, avg, 0.7, 5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.score_device(tc, tr, xy, mask, count, avg, 0.7, 5)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    print(f"skewed 2^18 batch (2 tiles): {ms:.2f} ms")
+    k = rng.choice(n, 4000, replace=False)
+    oxy, omask, ocount, oavg = orc.Scene(rgb, K, R, t).score_batch(c[k], ref[k], 0.7, 5, nthreads=8)
+    assert np.array_equal(mask.cpu().numpy()[k].view(np.uint64), omask)
+    assert np.array_equal(count.cpu().numpy()[k], ocount)
+    np.testing.assert_allclose(avg.cpu().numpy()[k], oavg, rtol=0, atol=AVG_TOL)
+    assert ms < 20.0
+
+
+def test_in_kernel_moments_path(pkg, dino, orc):
+    """The scorer without the per-scene window-moment tables (k_score_mma, the
+    path for scenes whose tables would not fit; MVS_SCORE_KERNEL=mma) against
+    the tables path and the oracle on the bench's candidates."""
+    import os
+    rgb, K, R, t = dino
+    c, ref = bench_candidates(1 << 17, K, R, t, seed=4)
+    os.environ["MVS_SCORE_KERNEL"] = "mma"
+    try:
+        cm = pkg.MvsContext(rgb, K, R, t, device=0)
+    finally:
+        del os.environ["MVS_SCORE_KERNEL"]
+    try:
+        cm.kernel_timing(True)
+        got = cm.score(c, ref, 0.7, 5)
+        cm.kernel_timing(False)
+        assert cm.timed_kernel() == "k_score_mma"
+    finally:
+        cm.close()
+    with pkg.MvsContext(rgb, K, R, t, device=0) as ct:
+        tab = ct.score(c, ref, 0.7, 5)
+    for g, e in zip(got[:3], tab[:3]):
+        assert np.array_equal(g, e)
+    np.testing.assert_allclose(got[3], tab[3], rtol=0, atol=AVG_TOL)
+    k = 5000
+    oxy, omask, ocount, oavg = orc.Scene(rgb, K, R, t).score_batch(c[:k], ref[:k], 0.7, 5, nthreads=8)
+    assert np.array_equal(got[1][:k], omask) and np.array_equal(got[2][:k], ocount)

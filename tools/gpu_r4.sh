@@ -21,3 +21,7 @@ import json,sys; d=json.loads(open('gpurun_out/${T}_b_$v.json').read().strip().s
 print('$v rep $rep: %.3f G cand/s  step %.1f us  kernel %.1f us (%s)  pack %.1f us' % (d['value']/1e9, d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, d['kernel'], d['exchange']['pack_us']))" | tee -a gpurun_out/${T}_ab.log
   done
 done
+if [ -z "$NO_STAMPS" ] && [ -f simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd/libmvs_amd_stamps.so ]; then
+  timeout -k 10 200 python tools/stamps_tab.py 5 > gpurun_out/${T}_stamps.log 2>&1 || { tail -5 gpurun_out/${T}_stamps.log; exit 1; }
+  grep -v amdgpu.ids gpurun_out/${T}_stamps.log
+fi

@@ -1,0 +1,41 @@
+"""Phase cycles of k_score_tab from the -DMVS_STAMPS diagnostic build
+(build_lib.py --stamps): per item and per wave, the barrier wait at the
+round's start, the wave's row-pair sort, its units (K-loops, epilogues)."""
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+
+import faulthandler
+faulthandler.dump_traceback_later(150, exit=True)   # a stuck run names its line
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+os.environ["MVS_LIB"] = os.environ.get("STAMPS_LIB") or os.path.join(
+    REPO, "simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd", "libmvs_amd_stamps.so")
+print("library", os.path.basename(os.environ["MVS_LIB"]))
+import bench  # noqa: E402
+
+wid = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+pkg = importlib.import_module(bench.PKG_NAME)
+n = 1 << 20
+rgb, K, R, t = bench.load_scene()
+c, ref = pkg.synthetic.candidates(n, K, R, t, seed=0)
+ctx = pkg.MvsContext(rgb, K, R, t)
+lib = pkg._lib.load()
+lib.mvs_read_stamps_tab.argtypes = [ctypes.c_void_p]
+buf = np.zeros(1024 * 16, np.uint64)
+ctx.score(c, ref, 0.7, wid)
+lib.mvs_read_stamps_tab(buf.ctypes.data)
+before = buf.copy()
+ctx.score(c, ref, 0.7, wid)
+lib.mvs_read_stamps_tab(buf.ctypes.data)
+d = (buf - before).reshape(1024, 16)[:512].astype(np.float64)
+items = d[:, 0].sum()
+waves = items * 8
+print(f"wid {wid}: items {items:.0f} over {(d[:, 0] > 0).sum()} workgroups; M-blocks {d[:, 4].sum():.0f}")
+for k, name in [(1, "barrier wait (round start)"), (2, "sort"), (3, "units"), (5, "  K-loops"), (6, "  epilogues")]:
+    print(f"  {name:28s} {d[:, k].sum() / waves:9.0f} cycles per (item, wave)")
+print(f"  per M-block: K-loop {d[:, 5].sum() / d[:, 4].sum():.0f}, epilogue {d[:, 6].sum() / d[:, 4].sum():.0f} cycles")
