@@ -112,9 +112,11 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
  * each) and |V| their popcount.
  * Device pointers, stream-ordered, no host synchronisation (the accepted
  * total is in the header; a slice with more than cap accepted keeps its
- * first cap).  accepted = -1 in the header means the pack's look-back gave
- * up (never expected; the rows are then incomplete): the consumer must
- * raise.  Feeds the all-gather of parallel.PointsExchange. */
+ * first cap).  The chunks' decoupled look-back never waits unboundedly: a
+ * wait that expires (another kernel holding the CUs) takes a slow path that
+ * counts the earlier candidates itself, so the rows are always exact;
+ * mvs_pack_fallbacks returns how often that happened (synchronises the
+ * device).  Feeds the all-gather of parallel.PointsExchange. */
 int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count,
                       const uint64_t* d_mask, const double* d_c, int vlb, int64_t cap, int64_t* d_out,
                       void* stream);
@@ -123,8 +125,10 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
  * 256-thread workgroups on `stream` -- the CU footprint of a collective's
  * kernel, run beside the scoring kernels on one GPU. */
 int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups, void* stream);
-/* Tests only: mode > 0 sets the pack's look-back spin limit, mode < 0 makes
- * chunk -mode (4096 candidates each) give up at once, 0 restores the default. */
+int64_t mvs_pack_fallbacks(mvs_ctx* ctx);
+/* Tests only: mode > 0 sets the pack's look-back spin limit, mode < 0 sends
+ * chunk -mode (4096 candidates each) down the slow path at once, 0 restores
+ * the default. */
 int mvs_pack_debug(mvs_ctx* ctx, int64_t mode);
 /* Kernel timing (measurement only): while enabled, every enable-th scoring
  * call (enable = 1: every call) records a HIP event pair on its stream

@@ -38,6 +38,7 @@ SIGNATURES = [
     ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
                                          ctypes.c_int64, _vp, _vp]),
     ("mvs_pack_debug", ctypes.c_int, [_vp, ctypes.c_int64]),
+    ("mvs_pack_fallbacks", ctypes.c_int64, [_vp]),
     ("mvs_proxy_copy", ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp]),
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
                                            _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
@@ -325,7 +326,7 @@ class MvsContext:
     def pack_accepted(self, offset, count, mask, vlb, out, stream=None, c=None):
         """mvs_pack_accepted: the accepted candidates (count >= vlb) of a scored
         slice as exchange rows of out (device int64 tensor (cap + 1, width):
-        row 0 = [accepted, n, 0...] (accepted = -1: the pack failed), then
+        row 0 = [accepted, n, 0...], then
         [offset + i, mask words(, x y z bits with c)] in index order); c = the
         slice's (n, 3) float64 centres or None (width 1 + words [+ 3]);
         stream-ordered, no host sync.  count None: mask is score_device_rec's
@@ -347,9 +348,17 @@ class MvsContext:
         check(rc, self._h, "mvs_pack_accepted")
 
     def pack_debug(self, mode=0):
-        """Tests only: the pack's look-back spin limit (mode > 0) or a forced
-        give-up of chunk -mode (mode < 0); 0 = default."""
+        """Tests only: the pack's look-back spin limit (mode > 0) or the slow
+        path for chunk -mode (mode < 0); 0 = default."""
         check(load().mvs_pack_debug(self._h, int(mode)), self._h, "mvs_pack_debug")
+
+    def pack_fallbacks(self):
+        """How many pack chunks took the slow (exact) path since the context
+        was created (synchronises the device)."""
+        r = int(load().mvs_pack_fallbacks(self._h))
+        if r < 0:
+            check(r, self._h, "mvs_pack_fallbacks")
+        return r
 
     def harris_points(self, view):
         """getHarrisPoints(imgs[view]) (HarrisFeatures.py:135-161) on the GPU:

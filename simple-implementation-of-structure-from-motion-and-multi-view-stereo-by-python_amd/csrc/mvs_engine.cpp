@@ -1473,10 +1473,8 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         ctx->scratch_acquire(s);
         const uint64_t* st_before = ctx->p_status.p;
-        // the chunks' words, then the two words of the finishing ticket
-        const int64_t nst = std::max<int64_t>((n + 4095) / 4096, 1);
-        ctx->p_status.ensure(nst + 2);
-        if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used; ticket 0
+        ctx->p_status.ensure(std::max<int64_t>((n + 4095) / 4096, 1));
+        if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used
             HIPCHK(hipMemsetAsync(ctx->p_status.p, 0, ctx->p_status.n * sizeof(uint64_t), s));
             ctx->p_epoch = 0;
         }
@@ -1485,10 +1483,7 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
             HIPCHK(hipMemsetAsync(ctx->p_err.p, 0, sizeof(int32_t), s));
         }
         ctx->p_epoch = ctx->p_epoch % ((1ull << 30) - 1) + 1;   // 1 .. 2^30 - 1
-        // the ticket words sit after every chunk word the buffer holds (its
-        // size only grows), so a later, larger slice never reads them as status
-        uint64_t* aux = ctx->p_status.p + ctx->p_status.n - 2;
-        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, d_c, ctx->words(), vlb, cap, ctx->p_status.p, aux,
+        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, d_c, ctx->words(), vlb, cap, ctx->p_status.p,
                                      ctx->p_epoch, ctx->p_err.p, ctx->pack_debug, d_out, s) != 0)
             throw Fail{MVS_E_HIP, "pack launch failed"};
         ctx->scratch_release(s);
@@ -1502,6 +1497,18 @@ int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups
     if (mvs_launch_proxy_copy(d_dst, d_src, bytes, workgroups, (hipStream_t)stream) != 0)
         return set_err(nullptr, Fail{MVS_E_HIP, "proxy copy launch failed"});
     return 0;
+}
+
+int64_t mvs_pack_fallbacks(mvs_ctx* ctx) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    int32_t h = 0;
+    int rc = guarded(ctx, [&]() {
+        if (!ctx->p_err.p) return 0;
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(&h, ctx->p_err.p, sizeof h, hipMemcpyDeviceToHost));
+        return 0;
+    });
+    return rc ? rc : h;
 }
 
 int mvs_pack_debug(mvs_ctx* ctx, int64_t mode) {

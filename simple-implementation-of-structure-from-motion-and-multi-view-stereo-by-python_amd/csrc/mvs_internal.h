@@ -180,14 +180,14 @@ int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hip
 // The accepted candidates of a sweep slice as exchange rows [global index,
 // mask words, (c != null) x y z bits] after a header row [accepted, n, 0...],
 // in index order, at most cap rows (parallel.PointsExchange), one launch;
-// status holds max(ceil(n / 4096), 1) words of the chunks' look-back, aux two
-// words (zero before the first launch: the finishing ticket, the total), epoch
-// in [1, 2^30) differs from the previous call's on the same status buffer,
-// *err counts look-back give-ups (reset by each launch's last chunk, which
-// then writes accepted = -1); debug: see k_acc_pack (0 in production)
+// count == null: mask holds records of words + 1 int64 and |V| is their
+// popcount; status holds max(ceil(n / 4096), 1) words of the chunks'
+// look-back, epoch in [1, 2^30) differs from the previous call's on the same
+// status buffer, *err counts look-back waits that expired and took the slow,
+// exact path; debug: see k_acc_pack (0 in production)
 int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, const double* c,
-                             int words, int vlb, int64_t cap, uint64_t* status, uint64_t* aux, uint64_t epoch,
-                             int32_t* err, int64_t debug, int64_t* out, hipStream_t s);
+                             int words, int vlb, int64_t cap, uint64_t* status, uint64_t epoch, int32_t* err,
+                             int64_t debug, int64_t* out, hipStream_t s);
 // measurement only: a copy of bytes (multiple of 16) by `workgroups` workgroups
 int mvs_launch_proxy_copy(void* dst, const void* src, int64_t bytes, int workgroups, hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,

@@ -1951,8 +1951,7 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // [accepted, n, 0...].  No host synchronisation: the accepted total travels in
 // the header, and a slice with more than cap accepted candidates keeps its
 // first cap rows (the receiver sees accepted > cap).  Each chunk's rows go to
-// (sum of the earlier chunks' counts) + their rank.  A failed look-back is
-// never silent: the header's accepted becomes -1 (PointsExchange.check raises).
+// (sum of the earlier chunks' counts) + their rank.
 // ---------------------------------------------------------------------------
 // Chunks of kAccPer x kAccThreads candidates, thread t of a chunk holding
 // candidates chunk + t + kAccThreads j (j < kAccPer): the count reads stay
@@ -1962,37 +1961,44 @@ constexpr int kAccThreads = 256, kAccPer = 16, kAccChunk = kAccThreads * kAccPer
 // One launch: each chunk's rows start after every earlier chunk's accepted
 // count, found by a decoupled look-back over per-chunk status words
 // (epoch << 34 | flag << 32 | value; flag 1 = the chunk's own count, 2 = the
-// inclusive count through it, 3 = poisoned: no valid prefix through it; a
-// word of another epoch is not yet published).  Workgroups are dispatched in
-// index order, so a chunk waits only for earlier chunks' workgroups, which
-// have started; a spin limit still bounds every wait -- a kernel sharing the
-// CUs (RCCL's, the next sweep's scorer) can delay them.  On expiry the chunk
-// counts one give-up in *err, writes no rows and publishes a poisoned word; a
-// chunk whose look-back ends on a poisoned word does the same.  The header is
-// written by the chunk that finishes last (a ticket in aux[0]; the last
-// chunk's total in aux[1]): accepted = -1 when any chunk gave up.  The words
-// are relaxed agent-scope atomics: a word carries all a reader needs, and a
-// release or acquire would write back or invalidate this XCD's L2 at every
-// step; the give-up count and the total are waited for (returning atomic /
-// s_waitcnt) before the chunk's ticket, so the last ticket sees them.
-// debug (tests only): > 0 = the spin limit; < 0 = chunk -debug gives up at once.
+// inclusive count through it; a word of another epoch is not yet published).
+// Workgroups are dispatched in index order, so a chunk waits only for earlier
+// chunks' workgroups, which have started; but a kernel sharing the CUs
+// (RCCL's, the next sweep's scorer) can delay them, so every wait is bounded:
+// on expiry the chunk takes the slow path that depends on no other workgroup
+// -- the whole workgroup counts the accepted candidates before it from the
+// inputs -- and publishes that exact prefix (so no result is ever wrong);
+// *err counts these fall-backs (mvs_pack_fallbacks).  The words are relaxed
+// agent-scope atomics: a word carries all a reader needs, and a release or
+// acquire would write back or invalidate this XCD's L2 at every step.
+// debug (tests only): > 0 = the spin limit; < 0 = chunk -debug falls back at once.
 constexpr int kAccGrid = 1024;
 constexpr uint32_t kAccSpin = 1u << 22;
+
+DEV int acc_count(const int32_t* __restrict__ count, const uint64_t* __restrict__ mask, int64_t ms, int words,
+                  int64_t i) {
+    if (count) return count[i];
+    int c = 0;
+    for (int q = 0; q < words; ++q) c += __popcll(mask[i * ms + q]);
+    return c;
+}
 
 __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
                                                           const uint64_t* __restrict__ mask, const double* __restrict__ cpt,
                                                           int words, int vlb, int64_t cap, uint64_t* __restrict__ status,
-                                                          uint64_t* __restrict__ aux, uint64_t epoch,
-                                                          int32_t* __restrict__ err, int64_t debug,
+                                                          uint64_t epoch, int32_t* __restrict__ err, int64_t debug,
                                                           int64_t* __restrict__ out) {
     __shared__ int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
-    __shared__ int64_t s_base;                        // -1: no valid prefix (this chunk writes no rows)
+    __shared__ int64_t s_base;
+    __shared__ int s_slow;
+    __shared__ int64_t s_total;
+    __shared__ int64_t s_part[kAccWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int width = 1 + words + (cpt ? 3 : 0);
     // count == null: the scorer's records [mask words, avg], |V| = popcount
     const int64_t ms = count ? words : words + 1;
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
-    const int64_t nch = nchunk > 0 ? nchunk : 1;      // an empty slice still has chunk 0
+    const int64_t nch = nchunk > 0 ? nchunk : 1;      // an empty slice still has chunk 0, which writes the header
     const uint64_t E = epoch << 34;
     const uint32_t spin_limit = debug > 0 ? (uint32_t)debug : kAccSpin;
     for (int64_t b = blockIdx.x; b < nch; b += gridDim.x) {
@@ -2002,15 +2008,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            int cc = 0;
-            if (i < n) {
-                if (count) {
-                    cc = count[i];
-                } else {
-                    for (int q = 0; q < words; ++q) cc += __popcll(mask[i * ms + q]);
-                }
-            }
-            c[j] = cc;
+            c[j] = i < n ? acc_count(count, mask, ms, words, i) : 0;
         }
         uint64_t m[kAccPer], w0[kAccPer];
 #pragma unroll
@@ -2040,25 +2038,20 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             uint64_t excl = 0;
             int64_t top = b - 1;          // the window's highest chunk
             uint32_t spins = 0;
-            bool poisoned = false, gave_up = debug < 0 && b == -debug;
-            while (top >= 0 && !gave_up) {
+            bool slow = debug < 0 && b == -debug;
+            while (top >= 0 && !slow) {
                 const int64_t k = top - lane;
                 uint64_t v = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                     : (E | (2ull << 32));
                 const bool pub = (v & ~((1ull << 34) - 1)) == E;
                 const uint32_t flag = pub ? (uint32_t)(v >> 32) & 3u : 0u;
-                // the nearest inclusive (or poisoned) word, and whether every
-                // chunk up to it has published
-                const uint64_t incl_m = __ballot(flag >= 2), unpub = __ballot(!pub);
+                // the nearest inclusive word, and whether every chunk up to it has published
+                const uint64_t incl_m = __ballot(flag == 2), unpub = __ballot(!pub);
                 const int first_incl = incl_m ? __builtin_ctzll(incl_m) : 64;
                 const int first_unpub = unpub ? __builtin_ctzll(unpub) : 64;
                 if (first_unpub < first_incl && first_unpub < 64) {
-                    if (++spins > spin_limit) gave_up = true;
+                    if (++spins > spin_limit) slow = true;
                     continue;                   // a chunk in the window has not published yet
-                }
-                if (first_incl < 64 && (__ballot(flag == 3) >> first_incl) & 1ull) {
-                    poisoned = true;            // the prefix through that chunk is unknown
-                    break;
                 }
                 // lanes 0..min(first_incl, 63) hold published words to sum
                 uint64_t val = (lane <= first_incl && k >= 0) ? (v & 0xffffffffull) : 0ull;
@@ -2069,60 +2062,69 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 top -= 64;
             }
             if (lane == 0) {
-                if (gave_up) {
-                    // counted (and waited for) before this chunk's ticket
-                    __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __builtin_amdgcn_s_waitcnt(0);
-                    poisoned = true;
+                if (!slow) {
+                    // the inclusive prefix, and the header from the last chunk
+                    if (b > 0)
+                        __hip_atomic_store(&status[b], E | (2ull << 32) | (excl + T), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    if (b == nch - 1) {
+                        out[0] = (int64_t)(excl + T);   // accepted in the whole slice
+                        out[1] = n;
+                        for (int q = 2; q < width; ++q) out[q] = 0;
+                    }
                 }
-                if (b > 0)
-                    __hip_atomic_store(&status[b], E | ((poisoned ? 3ull : 2ull) << 32) | (excl + T),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (b == nch - 1) {
-                    // the slice's total for the header (-1: unknown), performed
-                    // before this chunk's ticket
-                    __hip_atomic_store(&aux[1], poisoned ? ~0ull : (excl + T), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    __builtin_amdgcn_s_waitcnt(0);
-                }
-                s_base = poisoned ? -1 : (int64_t)excl;
+                s_slow = slow ? 1 : 0;
+                s_base = (int64_t)excl;
+                s_total = (int64_t)T;
             }
         }
         __syncthreads();
-        const int64_t base = s_base;
-        if (base >= 0) {
+        if (s_slow) {
+            // the slow path: the accepted candidates of [0, b chunk) counted
+            // from the inputs by the whole workgroup (no other workgroup involved)
+            int64_t part = 0;
+            for (int64_t i = threadIdx.x; i < b * kAccChunk; i += kAccThreads)
+                part += acc_count(count, mask, ms, words, i) >= vlb ? 1 : 0;
 #pragma unroll
-            for (int j = 0; j < kAccPer; ++j) {
-                if ((m[j] >> lane) & 1ull) {
-                    const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-                    const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
-                                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
-                    if (pos < cap) {
-                        int64_t* o = out + (1 + pos) * width;
-                        o[0] = offset + i;
-                        o[1] = (int64_t)w0[j];
-                        for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
-                        if (cpt) {
-                            // the accepted 3D point itself (binary64 bits)
-                            o[1 + words] = __double_as_longlong(cpt[3 * i]);
-                            o[2 + words] = __double_as_longlong(cpt[3 * i + 1]);
-                            o[3 + words] = __double_as_longlong(cpt[3 * i + 2]);
-                        }
+            for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+            if (lane == 0) s_part[wave] = part;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int64_t excl = 0;
+                for (int w = 0; w < kAccWaves; ++w) excl += s_part[w];
+                const int64_t T = s_total;
+                __hip_atomic_store(&status[b], E | (2ull << 32) | (uint64_t)(excl + T), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if (b == nch - 1) {
+                    out[0] = excl + T;
+                    out[1] = n;
+                    for (int q = 2; q < width; ++q) out[q] = 0;
+                }
+                s_base = excl;
+                __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+        }
+        const int64_t base = s_base;
+#pragma unroll
+        for (int j = 0; j < kAccPer; ++j) {
+            if ((m[j] >> lane) & 1ull) {
+                const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+                const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
+                                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
+                if (pos < cap) {
+                    int64_t* o = out + (1 + pos) * width;
+                    o[0] = offset + i;
+                    o[1] = (int64_t)w0[j];
+                    for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
+                    if (cpt) {
+                        // the accepted 3D point itself (binary64 bits)
+                        o[1 + words] = __double_as_longlong(cpt[3 * i]);
+                        o[2 + words] = __double_as_longlong(cpt[3 * i + 1]);
+                        o[3 + words] = __double_as_longlong(cpt[3 * i + 2]);
                     }
                 }
-            }
-        }
-        if (threadIdx.x == 0) {
-            // the chunk that finishes last writes the header
-            const uint64_t tk = __hip_atomic_fetch_add(&aux[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (tk == (uint64_t)(nch - 1)) {
-                const int gave = __hip_atomic_exchange(err, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t tot = __hip_atomic_load(&aux[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                out[0] = (gave != 0 || tot == ~0ull) ? -1 : (int64_t)tot;
-                out[1] = n;
-                for (int q = 2; q < width; ++q) out[q] = 0;
-                __hip_atomic_store(&aux[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
             }
         }
         __syncthreads();
@@ -2441,13 +2443,12 @@ extern "C" int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hip
 
 extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask,
                                         const double* c, int words, int vlb, int64_t cap, uint64_t* status,
-                                        uint64_t* aux, uint64_t epoch, int32_t* err, int64_t debug, int64_t* out,
-                                        hipStream_t s) {
+                                        uint64_t epoch, int32_t* err, int64_t debug, int64_t* out, hipStream_t s) {
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, kAccGrid));
     // n == 0 still writes the header (chunk 0 of an empty slice)
     hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, c, words, vlb, cap,
-                       status, aux, epoch, err, debug, out);
+                       status, epoch, err, debug, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -73,8 +73,7 @@ class PointsExchange:
     alternate; a pack waits for the all-gather that used its buffer two
     sweeps before.  cap = rows per rank (the bench takes the first sweep's
     accepted count plus a margin); a rank with more than cap accepted
-    candidates, or whose pack failed (header -1), shows it in its header
-    (check() and result() raise).
+    candidates shows it in its header (check() and result() raise).
 
     ctx = the rank's MvsContext (its pack kernel); on CPU tensors (gloo) the
     torch reference pack is used and the all-gather is synchronous."""
