@@ -417,8 +417,19 @@ def main():
     }
     out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms)
     if solo and not a.no_overlap:
-        out["exchange"]["overlap_proxy"] = overlap_proxy(ctx, sw, V, vlb, accepted, stream, a.thr, a.wid,
-                                                         max(a.steps // 2, 10))
+        ov = overlap_proxy(ctx, sw, V, vlb, accepted, stream, a.thr, a.wid, max(a.steps // 2, 10))
+        # the same with the scorer held to 448 workgroups (224 CUs), leaving
+        # 32 CUs to the collective's kernel
+        os.environ["MVS_SCORER_WGS"] = "448"
+        try:
+            ctx2 = pkg.MvsContext(rgb, K, R, t, device=local)
+        finally:
+            del os.environ["MVS_SCORER_WGS"]
+        ov["scorer_448_workgroups"] = {k: v for k, v in overlap_proxy(
+            ctx2, sw, V, vlb, accepted, stream, a.thr, a.wid, max(a.steps // 2, 10)).items()
+            if k.endswith("_us")}
+        ctx2.close()
+        out["exchange"]["overlap_proxy"] = ov
 
     if solo:
         # cold sweep: scene setup from the resident images + the sweep

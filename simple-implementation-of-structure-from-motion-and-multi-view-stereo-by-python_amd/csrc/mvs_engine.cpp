@@ -323,6 +323,7 @@ struct mvs_ctx {
     // (k_moments), rebuilt with the scene; tab_mode 0 = tables when they fit,
     // 1 = never (the in-kernel moments of k_score_mma; env MVS_SCORE_KERNEL=mma)
     int tab_mode = 0;
+    int scorer_wgs = 0;   // env MVS_SCORER_WGS: k_score_tab's grid (0 = every CU, twice)
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
     DevBuf<double> mom_w[MVS_MAX_WID + 1];
     bool mom_ok[MVS_MAX_WID + 1] = {};
@@ -519,6 +520,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         ctx->t_items.ensure((size_t)(n / std::max(t.chunk, 1) + ntiles + 2));
         t.items = ctx->t_items.p;
         t.zero_first = ctx->tiles_clean_ntiles != ntiles ? 1 : 0;
+        t.grid = ctx->scorer_wgs;
         ctx->tiles_clean_ntiles = -1;            // dirty until the sequence is queued
         hipEvent_t e0, e1;
         ctx->next_events(&e0, &e1);
@@ -1351,6 +1353,7 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
             else if (!std::strcmp(km, "tiled")) ctx->kernel_mode = 2;
             else if (!std::strcmp(km, "mma")) ctx->tab_mode = 1;   // tiled, in-kernel moments
         }
+        if (const char* sw = std::getenv("MVS_SCORER_WGS")) ctx->scorer_wgs = std::max(0, std::atoi(sw));
         return 0;
     });
     if (rc != 0) {

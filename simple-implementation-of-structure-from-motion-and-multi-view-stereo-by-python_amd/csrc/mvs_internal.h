@@ -89,6 +89,9 @@ struct TiledArgs {
     // sequence that did not complete)
     int zero_first;
     int4* items;
+    // workgroups of the persistent scorer (0: its default, every CU; fewer
+    // leave CUs free for a kernel that runs beside it, e.g. RCCL's)
+    int grid;
 };
 
 // Per-scene window moments of the tiled scorer (V <= 64), one table pair per

@@ -372,13 +372,26 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
     int tl[kBinPer], lr[kBinPer], pk[kBinPer];
+    // every candidate's inputs in flight at once (one memory round trip, not
+    // one per candidate)
+    int Rk[kBinPer];
+    double ck[kBinPer][3];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        const int64_t ii = i < a.n ? i : 0;
+        Rk[k] = a.ref[ii];
+        ck[k][0] = a.c[3 * ii];
+        ck[k][1] = a.c[3 * ii + 1];
+        ck[k][2] = a.c[3 * ii + 2];
+    }
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
         tl[k] = -1;
         if (i >= a.n) continue;
-        const int R = a.ref[i];
-        const double c[3] = {a.c[3 * i], a.c[3 * i + 1], a.c[3 * i + 2]};
+        const int R = Rk[k];
+        const double c[3] = {ck[k][0], ck[k][1], ck[k][2]};
         double px, py;
         project_vals(s_cam[R], c, px, py);
         a.xy[2 * i] = px;

@@ -13,6 +13,8 @@
 // tables, and the scorer k_score_tab only forms the window products S_ab on
 // the matrix cores (v_mfma_i32_16x16x64_i8 over the tile's staged region, as
 // k_score_mma does) and takes the decision num w_b > T from the tables.
+#include <algorithm>
+
 #include "mvs_device.h"
 #include "mvs_mma.h"
 
@@ -595,11 +597,12 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
 // hipFuncAttributeMaxDynamicSharedMemorySize is not needed: all LDS is static
 template <int WID, int NBLK>
 int launch_tab(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt, hipStream_t s) {
+    const dim3 grid(t->grid > 0 ? std::min(t->grid, kTabGrid) : kTabGrid);
     if (fabs(a->thr) >= 0.01)
-        hipLaunchKernelGGL((k_score_tab<WID, NBLK, true>), dim3(kTabGrid), dim3(kTabThreads), 0, s, *sc, *a, *t, *mt,
+        hipLaunchKernelGGL((k_score_tab<WID, NBLK, true>), grid, dim3(kTabThreads), 0, s, *sc, *a, *t, *mt,
                            (const int4*)t->items, (const int2*)t->sorted);
     else
-        hipLaunchKernelGGL((k_score_tab<WID, NBLK, false>), dim3(kTabGrid), dim3(kTabThreads), 0, s, *sc, *a, *t, *mt,
+        hipLaunchKernelGGL((k_score_tab<WID, NBLK, false>), grid, dim3(kTabThreads), 0, s, *sc, *a, *t, *mt,
                            (const int4*)t->items, (const int2*)t->sorted);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
