@@ -325,27 +325,36 @@ struct mvs_ctx {
     int tab_mode = 0;
     int scorer_wgs = 0;   // env MVS_SCORER_WGS: k_score_tab's grid (0 = every CU, twice)
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
-    DevBuf<double> mom_w[MVS_MAX_WID + 1];
+    DevBuf<double> mom_w[MVS_MAX_WID + 1];     // V <= 64
+    DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V > 64
     bool mom_ok[MVS_MAX_WID + 1] = {};
+    int moments_vp() const { return V > MVS_GROUP_VIEWS ? 64 * ((V + 63) / 64) : 16 * ((V + 15) / 16); }
     MomentsDev moments(int wid) const {
         MomentsDev m{};
         m.sb = mom_sb[wid].p;
         m.w = mom_w[wid].p;
-        m.VP = 16 * ((V + 15) / 16);
+        m.d = mom_d[wid].p;
+        m.VP = moments_vp();
         m.wid = wid;
         return m;
     }
-    // the tables of wid, built on stream s if needed; false when they do not
-    // apply (V > 64, disabled, or more than 2^31 elements)
+    // the tables of wid (10 B per (pixel, view) at V <= 64, 6 B above), built
+    // on stream s if needed; false when they do not apply (disabled, or more
+    // than 2^31 elements)
     bool ensure_moments(int wid, hipStream_t s) {
-        if (V > MVS_GROUP_VIEWS || tab_mode != 0) return false;
-        const int64_t elems = (int64_t)H * W * (16 * ((V + 15) / 16));
+        if (tab_mode != 0) return false;
+        const int64_t elems = (int64_t)H * W * moments_vp();
         if (elems >= ((int64_t)1 << 31)) return false;
         if (!mom_ok[wid]) {
             mom_sb[wid].alloc((size_t)elems);
-            mom_w[wid].alloc((size_t)elems);
             HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
-            HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
+            if (V > MVS_GROUP_VIEWS) {
+                mom_d[wid].alloc((size_t)elems);
+                HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
+            } else {
+                mom_w[wid].alloc((size_t)elems);
+                HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
+            }
             const MomentsDev m = moments(wid);
             if (mvs_launch_moments(&sc, &m, s) != 0) throw Fail{MVS_E_HIP, "moments launch failed"};
             mom_ok[wid] = true;
@@ -530,7 +539,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         const int rc = mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, tab ? &mt : nullptr, s, e0, e1);
         if (rc != 0) throw Fail{rc == -3 ? MVS_E_UNSUPPORTED : MVS_E_HIP, "tiled score launch failed"};
         ctx->scratch_release(s);
-        if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, tab ? 2 : 1);
+        if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, tab && !grouped ? 2 : 1);
         ctx->tiles_clean_ntiles = ntiles;        // k_score_fix leaves the counters zero
         return;
     }

@@ -94,16 +94,20 @@ struct TiledArgs {
     int grid;
 };
 
-// Per-scene window moments of the tiled scorer (V <= 64), one table pair per
-// window half-width, built once from the gray stack (k_moments) and read by
-// k_score_tab: for pixel (y, x) with a valid window and view v, element
-// (y * W + x) * VP + v holds S_b = the sum of the signed bytes s = g - 128
-// over the (2 wid + 1)^2 window (int16: |S_b| <= 121 * 128) and
-// w = 1 / sqrt(n S_bb - S_b^2) (v_rsq_f64 + one Newton step; nan for a
-// constant window and for the pad views V <= v < VP).  VP = 16 ceil(V / 16).
+// Per-scene window moments of the tiled scorers, one table pair per window
+// half-width, built once from the gray stack (k_moments): for pixel (y, x)
+// with a valid window and view v, element (y * W + x) * VP + v holds
+// S_b = the sum of the signed bytes s = g - 128 over the (2 wid + 1)^2 window
+// (int16: |S_b| <= 121 * 128) and
+//   V <= 64 (k_score_tab): w = 1 / sqrt(n S_bb - S_b^2) (v_rsq_f64 + one
+//     Newton step; nan for a constant window and for the pad views
+//     V <= v < VP), VP = 16 ceil(V / 16);
+//   V > 64 (k_score_mma_v): D = n S_bb - S_b^2 (int32, exact; -1 for the pad
+//     views), VP = 64 ceil(V / 64).
 struct MomentsDev {
     int16_t* sb;
-    double* w;
+    double* w;      // V <= 64
+    int32_t* d;     // V > 64
     int VP;
     int wid;
 };
@@ -162,6 +166,7 @@ int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledAr
 // the window-moment tables of one wid (mvs_score_tab.hip)
 int mvs_launch_moments(const SceneDev* sc, const MomentsDev* mt, hipStream_t s);
 // k_score_tab (V <= 64, the moments from the tables); k_bin has run
+// (V > 64: k_score_mma_v takes the tables through mvs_launch_score_tiled)
 int mvs_launch_score_tab(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt,
                          hipStream_t s);
 // dynamic LDS bytes of k_score_mma (0 if the configuration is unsupported)

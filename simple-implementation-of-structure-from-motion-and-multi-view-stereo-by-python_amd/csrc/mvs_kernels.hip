@@ -1224,10 +1224,11 @@ struct VLds {
     int qtab, ci, rmask, rguard, rsum, total;
 };
 
+template <bool TAB>
 __host__ __device__ constexpr VLds v_lds() {
     VLds L{};
-    L.qtab = 0;                                                 // [128 px][kVTab] int32
-    L.ci = L.qtab + 128 * kVTab * 4;
+    L.qtab = 0;                                                 // [128 px][kVTab] int32 (TAB: none)
+    L.ci = L.qtab + (TAB ? 0 : 128 * kVTab * 4);
     L.rmask = L.ci + kGroupChunk * (int)sizeof(CandInfoV);      // [cand][4 view blocks] u16 (item start:
                                                                 // [cand] {S_a, S_aa} int32 sums)
     L.rguard = L.rmask + kGroupChunk * 4 * 2;                   // [cand][2 halves] u16
@@ -1268,9 +1269,9 @@ DEV double rsqrt_nr(int D) {
     return w;
 }
 
-template <int WID, bool FAST>
+template <int WID, bool FAST, bool TAB>
 __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
-                                                             const int4* __restrict__ items,
+                                                             const MomentsDev mt, const int4* __restrict__ items,
                                                              const int2* __restrict__ sorted) {
     using G = MmaGeom<WID>;
     constexpr int NB = G::NB, NPX = G::NPX, ROWS = G::ROWS, VS = G::VS, C0 = G::C0;
@@ -1295,7 +1296,10 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     __shared__ int s_item;
     __shared__ __attribute__((aligned(16))) int32_t s_cnt[16];   // the sort's per-wave row counts
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr VLds L = v_lds();
+    constexpr VLds L = v_lds<TAB>();
+    const int16_t* __restrict__ tsb = mt.sb;   // TAB: S_b and D = n S_bb - S_b^2 per (pixel, view)
+    const int32_t* __restrict__ tdd = mt.d;
+    const int VPt = mt.VP;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int V = sc.V;
@@ -1461,10 +1465,12 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             int claim = 0;
             if (g == 0 && tid == 0) claim = atomicAdd(head, 1);
             // ---- 2. Q = S_bb of every (pixel, view) of the group ----
+            // (TAB: none, the scene's tables hold S_b and D)
 #ifdef MVS_DIAG_NOPHASE2
             if (false) {
 #else
-            if (mv < GV) {
+            if (TAB) {
+            } else if (mv < GV) {
 #endif
                 // rows in order, the window sliding down as they come: at most
                 // NB + 1 row sums live
@@ -1488,6 +1494,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
 #pragma unroll
                 for (int y = 0; y < MVS_TILE_H; ++y) qtab[(y * 16 + mx) * kVTab + mv] = -1;   // D < 0: nan
             }
+            (void)mx; (void)mv; (void)cmk; (void)cd0;
             STAMP(t0a);
             // (and, group 0, the reference rows have landed; nothing else is in
             // flight, so the LDS reads of phases 3-4 need no waits)
@@ -1533,7 +1540,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                     const int s = asums[2 * tid], q = asums[2 * tid + 1];
                     const double wa = rsqrt_nr(NPX * q - s * s);
                     CandInfoV c;
-                    c.px = (pk & 127) * kVTab;
+                    // the pixel's row: of the Q table, or (TAB) of the scene's tables
+                    c.px = TAB ? ((ty * MVS_TILE_H + ((pk >> 4) & 7)) * sc.W + x0 + (pk & 15)) * VPt
+                               : (pk & 127) * kVTab;
                     c.R = pk >> 7;
                     c.Sa = -s;
                     c.pk = pk;
@@ -1600,8 +1609,12 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                     const v4i B1 = {(int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
                     C0v = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B0, C0v, 0, 0, 0);
                     C1v = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B1, C1v, 0, 0, 0);
-                    S0v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B0, S0v, 0, 0, 0);
-                    S1v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B1, S1v, 0, 0, 0);
+                    if constexpr (!TAB) {
+                        S0v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B0, S0v, 0, 0, 0);
+                        S1v = __builtin_amdgcn_mfma_i32_16x16x64_i8(AI, B1, S1v, 0, 0, 0);
+                    } else {
+                        (void)AI;
+                    }
                 };
                 // every window takes KMIN K-steps: those unrolled from sb (loads
                 // issued ahead of the MFMAs), the block's further ones after
@@ -1613,16 +1626,33 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 // lane (kh, m) holds candidate 16 b + 4 kh + i, views vb + 32 h + 16 j + m
                 uint32_t pmv = 0, gdv = 0;
                 double sacc[4];
+                // TAB: S_b and D of candidate 4 kh + i's pixel at views vb + 32 h +
+                // 16 j + m from the tables, one candidate step ahead of their use
+                int tsbv[2][2], tdv[2][2];
+                auto tfetch = [&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (TAB) {
+                        const int px = ci[min(b * 16 + 4 * kh + i, nc - 1)].px + vb + 32 * h + m;
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            tsbv[i & 1][j] = tsb[px + 16 * j];
+                            tdv[i & 1][j] = tdd[px + 16 * j];
+                        }
+                    }
+                };
+                tfetch(std::integral_constant<int, 0>{});
                 static_for<4>([&](auto Ic) {
                     constexpr int i = Ic;
+                    if constexpr (i < 3) tfetch(std::integral_constant<int, i + 1>{});
                     const CandInfoV c = ci[min(b * 16 + 4 * kh + i, nc - 1)];
                     double sa = 0.0;
                     uint64_t gacc = 0;
                     static_for<2>([&](auto Jc) {
                         constexpr int j = Jc;
                         const int vl = 32 * h + 16 * j + m;
-                        const int Sb = j ? S1v[i] : S0v[i];
-                        const int D = __mul24(NPX, qtab[c.px + vl]) - __mul24(Sb, Sb);   // < 0 past V: nan
+                        const int Sb = TAB ? tsbv[i & 1][j] : (j ? S1v[i] : S0v[i]);
+                        const int D = TAB ? tdv[i & 1][j]
+                                          : __mul24(NPX, qtab[c.px + vl]) - __mul24(Sb, Sb);   // < 0 past V: nan
                         const float wf = __builtin_amdgcn_rsqf((float)D);
                         const int num = __mul24(c.Sa, Sb) + __mul24(NPX, j ? C1v[i] : C0v[i]);
                         const uint64_t liv = __builtin_amdgcn_uicmp((uint32_t)(vb + vl), (uint32_t)c.R, 33);
@@ -2270,18 +2300,34 @@ inline int set_dyn_lds_once(const void* f, std::atomic<uint64_t>& done, int lds)
 }
 
 template <int WID, int NBLK, bool GROUPED>
-int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, hipStream_t s) {
-    static std::atomic<uint64_t> attr_fast{0}, attr_slow{0};
+int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt, hipStream_t s) {
+    static std::atomic<uint64_t> attr_fast{0}, attr_slow{0}, attr_fast2{0}, attr_slow2{0};
     if constexpr (GROUPED) {
-        constexpr int lds = v_lds().total;
-        if (fabs(a->thr) >= 0.01) {
-            if (set_dyn_lds_once((const void*)k_score_mma_v<WID, true>, attr_fast, lds) != 0) return -1;
-            hipLaunchKernelGGL((k_score_mma_v<WID, true>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc, *a, *t,
-                               (const int4*)t->items, (const int2*)t->sorted);
+        // (mt: the scene's S_b / D tables, or null: the Q table per item and group)
+        const MomentsDev m0{};
+        const MomentsDev& m = mt ? *mt : m0;
+        if (mt) {
+            constexpr int lds = v_lds<true>().total;
+            if (fabs(a->thr) >= 0.01) {
+                if (set_dyn_lds_once((const void*)k_score_mma_v<WID, true, true>, attr_fast, lds) != 0) return -1;
+                hipLaunchKernelGGL((k_score_mma_v<WID, true, true>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc,
+                                   *a, *t, m, (const int4*)t->items, (const int2*)t->sorted);
+            } else {
+                if (set_dyn_lds_once((const void*)k_score_mma_v<WID, false, true>, attr_slow, lds) != 0) return -1;
+                hipLaunchKernelGGL((k_score_mma_v<WID, false, true>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc,
+                                   *a, *t, m, (const int4*)t->items, (const int2*)t->sorted);
+            }
         } else {
-            if (set_dyn_lds_once((const void*)k_score_mma_v<WID, false>, attr_slow, lds) != 0) return -1;
-            hipLaunchKernelGGL((k_score_mma_v<WID, false>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc, *a, *t,
-                               (const int4*)t->items, (const int2*)t->sorted);
+            constexpr int lds = v_lds<false>().total;
+            if (fabs(a->thr) >= 0.01) {
+                if (set_dyn_lds_once((const void*)k_score_mma_v<WID, true, false>, attr_fast2, lds) != 0) return -1;
+                hipLaunchKernelGGL((k_score_mma_v<WID, true, false>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc,
+                                   *a, *t, m, (const int4*)t->items, (const int2*)t->sorted);
+            } else {
+                if (set_dyn_lds_once((const void*)k_score_mma_v<WID, false, false>, attr_slow2, lds) != 0) return -1;
+                hipLaunchKernelGGL((k_score_mma_v<WID, false, false>), dim3(kMmaGrid), dim3(kMmaThreads), lds, s, *sc,
+                                   *a, *t, m, (const int4*)t->items, (const int2*)t->sorted);
+            }
         }
     } else {
         // the largest table is sized for V = 16 NBLK; every V of this NBLK fits in it
@@ -2323,13 +2369,13 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     int rc = 0;
     {
         TimedLaunch tl(s, ev0, ev1);
-        if (grouped) rc = launch_mma<WID, 4, true>(sc, a, t, s);
+        if (grouped) rc = launch_mma<WID, 4, true>(sc, a, t, mt, s);
         else if (mt) rc = mvs_launch_score_tab(sc, a, t, mt, s);   // window moments from the scene's tables
         else switch ((sc->V + 15) / 16) {
-            case 1: rc = launch_mma<WID, 1, false>(sc, a, t, s); break;
-            case 2: rc = launch_mma<WID, 2, false>(sc, a, t, s); break;
-            case 3: rc = launch_mma<WID, 3, false>(sc, a, t, s); break;
-            default: rc = launch_mma<WID, 4, false>(sc, a, t, s); break;
+            case 1: rc = launch_mma<WID, 1, false>(sc, a, t, nullptr, s); break;
+            case 2: rc = launch_mma<WID, 2, false>(sc, a, t, nullptr, s); break;
+            case 3: rc = launch_mma<WID, 3, false>(sc, a, t, nullptr, s); break;
+            default: rc = launch_mma<WID, 4, false>(sc, a, t, nullptr, s); break;
         }
     }
     if (rc) return rc;
@@ -2394,7 +2440,7 @@ extern "C" int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid,
 
 template <int WID>
 size_t mma_lds_bytes_w(int V) {
-    if (V > kGroupViews) return (size_t)(v_lds().total + v_static_lds<WID>());
+    if (V > kGroupViews) return (size_t)(v_lds<false>().total + v_static_lds<WID>());
     switch ((V + 15) / 16) {
         case 1: return (size_t)mma_layout<WID, 1>(V).total;
         case 2: return (size_t)mma_layout<WID, 2>(V).total;

@@ -34,7 +34,7 @@ namespace {
 // ---------------------------------------------------------------------------
 constexpr int kMomW = 32, kMomH = 16, kMomV = 16;
 
-template <int WID>
+template <int WID, bool DTAB>
 __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const MomentsDev mt) {
     constexpr int NB = 2 * WID + 1, NPX = NB * NB;
     constexpr int ROWS = kMomH + 2 * WID, COLS = kMomW + 2 * WID, CP = (COLS + 3) & ~3;
@@ -94,14 +94,19 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
             const int64_t o = ((int64_t)y * sc.W + x) * mt.VP + v0 + vi;
             if (vi < nv) {
                 const int db = NPX * Q - S * S;
-                const double D = (double)db;
-                double w = __builtin_amdgcn_rsq(D);
-                w = w * (1.5 - 0.5 * D * w * w);
                 mt.sb[o] = (int16_t)(S - 128 * NPX);
-                mt.w[o] = w;
+                if constexpr (DTAB) {
+                    mt.d[o] = db;
+                } else {
+                    const double D = (double)db;
+                    double w = __builtin_amdgcn_rsq(D);
+                    w = w * (1.5 - 0.5 * D * w * w);
+                    mt.w[o] = w;
+                }
             } else {
                 mt.sb[o] = 0;
-                mt.w[o] = __builtin_nan("");
+                if constexpr (DTAB) mt.d[o] = -1;
+                else mt.w[o] = __builtin_nan("");
             }
         }
     }
@@ -626,17 +631,25 @@ extern "C" int mvs_read_stamps_tab(unsigned long long* out) {
 #endif
 
 extern "C" int mvs_launch_moments(const SceneDev* sc, const MomentsDev* mt, hipStream_t s) {
-    if (sc->V > 64 || mt->VP != 16 * ((sc->V + 15) / 16)) return -3;
+    const bool dtab = sc->V > 64;
+    if (mt->VP != (dtab ? 64 * ((sc->V + 63) / 64) : 16 * ((sc->V + 15) / 16))) return -3;
     const dim3 grid((unsigned)((sc->W + kMomW - 1) / kMomW), (unsigned)((sc->H + kMomH - 1) / kMomH),
                     (unsigned)(mt->VP / kMomV));
+#define MVS_MOM(W_) (dtab ? (const void*)k_moments<W_, true> : (const void*)k_moments<W_, false>)
+    const void* f = nullptr;
     switch (mt->wid) {
-        case 1: hipLaunchKernelGGL(k_moments<1>, grid, dim3(256), 0, s, *sc, *mt); break;
-        case 2: hipLaunchKernelGGL(k_moments<2>, grid, dim3(256), 0, s, *sc, *mt); break;
-        case 3: hipLaunchKernelGGL(k_moments<3>, grid, dim3(256), 0, s, *sc, *mt); break;
-        case 4: hipLaunchKernelGGL(k_moments<4>, grid, dim3(256), 0, s, *sc, *mt); break;
-        case 5: hipLaunchKernelGGL(k_moments<5>, grid, dim3(256), 0, s, *sc, *mt); break;
+        case 1: f = MVS_MOM(1); break;
+        case 2: f = MVS_MOM(2); break;
+        case 3: f = MVS_MOM(3); break;
+        case 4: f = MVS_MOM(4); break;
+        case 5: f = MVS_MOM(5); break;
         default: return -2;
     }
+#undef MVS_MOM
+    const SceneDev scv = *sc;
+    const MomentsDev mtv = *mt;
+    void* args[] = {(void*)&scv, (void*)&mtv};
+    if (hipLaunchKernel(f, grid, dim3(256), args, 0, s) != hipSuccess) return -1;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
