@@ -37,25 +37,31 @@ constexpr int kMomW = 32, kMomH = 16, kMomV = 16;
 template <int WID, bool DTAB>
 __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const MomentsDev mt) {
     constexpr int NB = 2 * WID + 1, NPX = NB * NB;
-    constexpr int ROWS = kMomH + 2 * WID, COLS = kMomW + 2 * WID, CP = (COLS + 3) & ~3;
-    __shared__ __attribute__((aligned(16))) uint8_t g[kMomV][ROWS][CP];
+    // LDS column c holds image column x0 - 8 + c: 48 bytes cover the block's
+    // 32 columns and both window halos (WID <= 5 < 8)
+    constexpr int ROWS = kMomH + 2 * WID, CP = 48, CW = CP / 4;
+    __shared__ __attribute__((aligned(16))) uint32_t g4[kMomV][ROWS][CW];
     __shared__ uint32_t hs[kMomV][ROWS][kMomW];
     const int x0 = blockIdx.x * kMomW, y0 = blockIdx.y * kMomH, v0 = blockIdx.z * kMomV;
     const int tid = threadIdx.x;
     const int nv = min(kMomV, sc.V - v0);
-    // the bytes: gv rows (signed s = g - 128, 8 pad bytes left of column 0 and
-    // >= 24 right of W-1); rows outside the image clamped (never in a valid
-    // window); views past V zero
-    for (int k = tid; k < kMomV * ROWS * COLS; k += 256) {
-        const int vi = k / (ROWS * COLS), rc = k - vi * (ROWS * COLS), r = rc / COLS, c = rc - r * COLS;
+    // the bytes, one dword per thread and step, coalesced along each row: gv
+    // rows (signed s = g - 128; 8 pad bytes left of column 0 and >= 24 right
+    // of W-1, so [x0 - 8, x0 + 40) is inside the row's pitch or, for the last
+    // columns, the next row's start / the buffer's 64-byte tail, never used
+    // by a valid window); rows outside the image clamped; views past V zero
+    for (int k = tid; k < kMomV * ROWS * CW; k += 256) {
+        const int vi = k / (ROWS * CW), rc = k - vi * (ROWS * CW), r = rc / CW, c = rc - r * CW;
         const int y = min(max(y0 - WID + r, 0), sc.H - 1);
-        const int x = min(max(x0 - WID + c, -8), sc.W + 23);
-        g[vi][r][c] = vi < nv ? (uint8_t)(sc.gv[((int64_t)(v0 + vi) * sc.H + y) * sc.Wp + x] ^ 0x80) : (uint8_t)0;
+        uint32_t wv = 0u;
+        if (vi < nv)
+            wv = *(const uint32_t*)(sc.gv + ((int64_t)(v0 + vi) * sc.H + y) * sc.Wp + x0 - 8 + 4 * c) ^ 0x80808080u;
+        g4[vi][r][c] = wv;
     }
     __syncthreads();
     for (int k = tid; k < kMomV * ROWS; k += 256) {
         const int vi = k / ROWS, r = k - vi * ROWS;
-        const uint8_t* row = g[vi][r];
+        const uint8_t* row = (const uint8_t*)g4[vi][r] + 8 - WID;   // image column x0 - WID
         uint32_t S = 0, Q = 0;
 #pragma unroll
         for (int c = 0; c < NB; ++c) {
