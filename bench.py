@@ -169,10 +169,10 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
     pc, pm = pack_src(sw)
     for _ in range(3):
         ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
-    # device time: the packs queue up behind three sweeps' worth of scoring,
-    # so the host's submission rate (a ctypes call + two launches per pack,
-    # ~15 us) does not pace them
-    for _ in range(3):
+    # device time: the packs queue up behind ten sweeps' worth of scoring
+    # (~1 ms), so the host's submission rate (a ctypes call and a launch per
+    # pack, ~15 us) does not pace them
+    for _ in range(10):
         score(ctx, sw, wid, thr, stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -187,7 +187,7 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
             "received_per_rank_at_n8_MB": 7 * row * (cap + 1) / 1e6,
             "note": "rows [global index, mask word, x, y, z]: the accepted 3D points themselves; "
                     "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync), device time "
-                    "of 20 packs queued behind scoring work; the "
+                    "of 20 packs queued behind ten sweeps of scoring work; the "
                     "all-gather runs on its own stream behind the next sweep (parallel.PointsExchange)"}
 
 

@@ -59,8 +59,8 @@ struct ScoreArgs {
 };
 
 // Scratch of the tiled scorer (device pointers, sized by the host).
-//   tile_count[ntiles+4]: per-tile counts, then the queue head, fix_count,
-//   n_items, done (k_score_fix's finishing ticket)
+//   tile_count[ntiles+12]: per-tile counts, then the queue head, fix_count,
+//   n_items, done (k_score_fix's finishing ticket), 8 per-XCD queue heads
 //   sorted[ntiles*cap] = {id, pk} per tile bucket (k_bin writes candidate
 //   rank r of tile k at k*cap + r), pk = (x - x0) | (y - y0) << 4 | R << 7
 //   (pixel inside the tile); a candidate of rank >= cap overflows to fix_list

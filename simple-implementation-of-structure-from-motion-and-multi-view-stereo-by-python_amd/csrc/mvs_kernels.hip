@@ -1789,6 +1789,7 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
         *t.fix_count = 0;
         *t.n_items = 0;
         t.tile_count[t.ntiles] = 0;   // the queue head
+        for (int l = 0; l < 8; ++l) t.tile_count[t.ntiles + 4 + l] = 0;   // the per-XCD heads (MVS_XCD_QUEUE)
         *t.done = 0;
     }
 }
@@ -2358,7 +2359,7 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     // tile counters, the work-queue head (tile_count[ntiles]) and fix_count:
     // left at zero by the previous batch's item scan unless zero_first
     if (t->zero_first &&
-        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 4), s) != hipSuccess)
+        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 12), s) != hipSuccess)
         return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);

@@ -244,11 +244,33 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
         }
     };
 
+#ifdef MVS_XCD_QUEUE
+    // XCD-aware queue (A/B switch): the item list in 8 contiguous ranges, one
+    // per workgroup label blockIdx % 8 (workgroups b and b + 8 share an XCD as
+    // dispatched, so a range's tiles -- and their overlapping regions -- meet
+    // in one L2); a label's workgroups take its range first, then the others'
+    // (thread 0 remembers the exhausted ranges); placement changes only speed
+    int32_t* heads = &t.tile_count[t.ntiles + 4];
+    uint32_t dead = 0;
+    auto claim = [&]() -> int {
+        for (int k = 0; k < 8; ++k) {
+            const int l = (blockIdx.x + k) & 7;
+            if ((dead >> l) & 1u) continue;
+            const int b = (int)((int64_t)n_units * l / 8), e = (int)((int64_t)n_units * (l + 1) / 8);
+            const int v = b < e ? atomicAdd(&heads[l], 1) : e;
+            if (b + v < e) return b + v;
+            dead |= 1u << l;
+        }
+        return n_units;
+    };
+#else
+    auto claim = [&]() -> int { return atomicAdd(head, 1); };
+#endif
     // the item pipeline: while item k is scored, item k+1's region and list
     // (DB), item k+2's descriptor and thread 0's claim of item k+3 are in flight
     if (tid == 0) {
-        s_ids[0] = atomicAdd(head, 1);
-        s_ids[1] = atomicAdd(head, 1);
+        s_ids[0] = claim();
+        s_ids[1] = claim();
     }
     __syncthreads();
     int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     stage(dcur, std::integral_constant<int, 0>{});
     int4 dnx1 = nx1 < n_units ? item_desc(t, items, nx1) : make_int4(0, 0, 0, 0);
     int pend = 0;
-    if (tid == 0) pend = atomicAdd(head, 1);
+    if (tid == 0) pend = claim();
     __syncthreads();   // everyone has read s_ids before they are rewritten
 
     auto round = [&](auto bufc) -> bool {
@@ -283,7 +305,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
         int4 dnx2 = make_int4(0, 0, 0, 0);
         if (nx2 < n_units) {
             dnx2 = item_desc(t, items, nx2);
-            if (tid == 0) pend = atomicAdd(head, 1);
+            if (tid == 0) pend = claim();
         }
         const int ty = dcur.x / t.ntx, tx = dcur.x - ty * t.ntx;
         const int tix0 = ((ty * MVS_TILE_H) * sc.W + tx * MVS_TILE_W) * VP;   // table element of the tile origin

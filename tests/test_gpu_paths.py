@@ -324,9 +324,9 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
         cc = tc if pts else None
         for _ in range(3):
             ctx.pack_accepted(0, count, mask, 3, out, stream=s.cuda_stream, c=cc)
-        # the packs queue behind scoring work, so that the events time the device
-        # and not the host's submission rate (~15 us per ctypes call + 2 launches)
-        for _ in range(3):
+        # the packs queue behind scoring work (~1 ms of it), so that the events
+        # time the device and not the host's submission rate (~15 us per call)
+        for _ in range(10):
             ctx.score_device(tc, tr, xy, mask, count, None, 0.7, 5, stream=s.cuda_stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)

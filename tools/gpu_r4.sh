@@ -13,9 +13,10 @@ fi
 B="--no-stage --no-ring --secondary-wid 0 --steps 100 --no-cpu-baseline ${BENCH_ARGS}"
 : > gpurun_out/${T}_ab.log
 for rep in 1 2; do
-  for v in tab mma; do
-    if [ $v = mma ]; then KM=mma; else KM=; fi
-    MVS_SCORE_KERNEL=$KM timeout -k 10 200 python bench.py $B > gpurun_out/${T}_b_$v.json 2>gpurun_out/${T}_b.err || { tail -5 gpurun_out/${T}_b.err; exit 1; }
+  for v in tab ${NO_MMA:-mma} ${VARIANTS}; do
+    KM=; L=$PWD/simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd/libmvs_amd.so
+    if [ $v = mma ]; then KM=mma; elif [ $v != tab ]; then L=${L%.so}_$v.so; fi
+    MVS_LIB=$L MVS_SCORE_KERNEL=$KM timeout -k 10 200 python bench.py $B > gpurun_out/${T}_b_$v.json 2>gpurun_out/${T}_b.err || { tail -5 gpurun_out/${T}_b.err; exit 1; }
     python -c "
 import json,sys; d=json.loads(open('gpurun_out/${T}_b_$v.json').read().strip().splitlines()[-1])
 print('$v rep $rep: %.3f G cand/s  step %.1f us  kernel %.1f us (%s)  pack %.1f us' % (d['value']/1e9, d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, d['kernel'], d['exchange']['pack_us']))" | tee -a gpurun_out/${T}_ab.log
