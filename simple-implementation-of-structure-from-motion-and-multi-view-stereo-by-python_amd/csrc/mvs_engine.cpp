@@ -307,7 +307,7 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand;
-    // mvs_pack_accepted: the chunks' look-back words (one per 4096
+    // mvs_pack_accepted: the chunks' look-back words (one per MVS_ACC_CHUNK
     // candidates), their epoch and the give-up counter
     DevBuf<uint64_t> p_status;
     DevBuf<int32_t> p_err;
@@ -1485,7 +1485,7 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
         ctx->scratch_acquire(s);
         const uint64_t* st_before = ctx->p_status.p;
-        ctx->p_status.ensure(std::max<int64_t>((n + 4095) / 4096, 1));
+        ctx->p_status.ensure(std::max<int64_t>((n + MVS_ACC_CHUNK - 1) / MVS_ACC_CHUNK, 1));
         if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used
             HIPCHK(hipMemsetAsync(ctx->p_status.p, 0, ctx->p_status.n * sizeof(uint64_t), s));
             ctx->p_epoch = 0;

@@ -149,6 +149,7 @@ struct ExpandArgs {
 #define MVS_MMA_CHUNK 1024    // candidates per work item, V <= 64 (whole tiles, as a rule)
 #define MVS_GROUP_VIEWS 64    // views per group when V > 64
 #define MVS_GROUP_CHUNK 116   // candidates per work item when V > 64 (their reference rows staged)
+#define MVS_ACC_CHUNK 16384   // candidates per chunk of the exchange's pack (k_acc_pack)
 
 extern "C" {
 // RGB -> stack and gv (one pass, coalesced on both sides); the caller zeroes
@@ -189,7 +190,7 @@ int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hip
 // mask words, (c != null) x y z bits] after a header row [accepted, n, 0...],
 // in index order, at most cap rows (parallel.PointsExchange), one launch;
 // count == null: mask holds records of words + 1 int64 and |V| is their
-// popcount; status holds max(ceil(n / 4096), 1) words of the chunks'
+// popcount; status holds max(ceil(n / MVS_ACC_CHUNK), 1) words of the chunks'
 // look-back, epoch in [1, 2^30) differs from the previous call's on the same
 // status buffer, *err counts look-back waits that expired and took the slow,
 // exact path; debug: see k_acc_pack (0 in production)

@@ -1304,7 +1304,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int V = sc.V;
     const int NG = t.groups;
-    const int words = (V + 63) >> 6;
     int32_t* qtab = (int32_t*)(smem + L.qtab);
     CandInfoV* ci = (CandInfoV*)(smem + L.ci);
     uint16_t* rmask = (uint16_t*)(smem + L.rmask);
@@ -1771,7 +1770,6 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
     const int nfix = *t.fix_count;
     const int active = nfix > kFixSmall ? (int)gridDim.x : kFixBase;   // uniform over the grid
     if ((int)blockIdx.x >= active) return;
-    const int words = (sc.V + 63) >> 6;
     for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += active * 256) t.tile_count[k] = 0;
     for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
          k += active * 4) {
@@ -1997,10 +1995,15 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // first cap rows (the receiver sees accepted > cap).  Each chunk's rows go to
 // (sum of the earlier chunks' counts) + their rank.
 // ---------------------------------------------------------------------------
-// Chunks of kAccPer x kAccThreads candidates, thread t of a chunk holding
-// candidates chunk + t + kAccThreads j (j < kAccPer): the count reads stay
-// coalesced and a workgroup does enough work to hide its latency.
-constexpr int kAccThreads = 256, kAccPer = 16, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
+// Chunks of kAccPer x kAccThreads = 16,384 candidates, thread t of a chunk
+// holding candidates chunk + t + kAccThreads j (j < kAccPer): the count reads
+// stay coalesced, a workgroup has enough loads in flight to hide their
+// latency, and a 2^20 slice has 64 chunks -- one look-back window, so a
+// chunk's prefix is one round of status loads behind its predecessors' own
+// counts (4,096-candidate chunks: up to four windows walked in turn).
+constexpr int kAccThreads = 1024, kAccPer = 16, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
+static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the status words by MVS_ACC_CHUNK");
+static_assert(kAccPer * kAccWaves == 256, "wave 0 scans the (j, wave) counts four per lane");
 
 // One launch: each chunk's rows start after every earlier chunk's accepted
 // count, found by a decoupled look-back over per-chunk status words
@@ -2032,7 +2035,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                                                           int words, int vlb, int64_t cap, uint64_t* __restrict__ status,
                                                           uint64_t epoch, int32_t* __restrict__ err, int64_t debug,
                                                           int64_t* __restrict__ out) {
-    __shared__ int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
+    __shared__ __attribute__((aligned(16))) int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
     __shared__ int64_t s_base;
     __shared__ int s_slow;
     __shared__ int64_t s_total;
@@ -2065,15 +2068,18 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
         }
         __syncthreads();
         if (wave == 0) {
-            // exclusive scan of the (j, wave) counts in index order
-            const int x = s_cnt[lane];
-            int incl = x;
+            // exclusive scan of the 256 (j, wave) counts in index order, four
+            // consecutive ones per lane
+            const int4 x4 = ((const int4*)s_cnt)[lane];
+            const int l1 = x4.x + x4.y, l2 = l1 + x4.z, tot = l2 + x4.w;
+            int incl = tot;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
                 const int y = __shfl_up(incl, off, 64);
                 if (lane >= off) incl += y;
             }
-            s_cnt[lane] = incl - x;
+            const int ex = incl - tot;
+            ((int4*)s_cnt)[lane] = make_int4(ex, ex + x4.x, ex + l1, ex + l2);
             const uint64_t T = (uint32_t)__shfl(incl, 63, 64);   // this chunk's accepted
             // publish, then look back over the 64 chunks before b at a time
             if (lane == 0)

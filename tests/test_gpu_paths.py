@@ -341,13 +341,14 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
             assert us <= 10.0
 
 
-@pytest.mark.parametrize("n", [1, 4095, 4097, 5_000_001])
+@pytest.mark.parametrize("n", [1, 16383, 16385, 5_000_001, 21_000_001])
 def test_pack_accepted_lookback_sizes(pkg, ctx, n):
-    """The pack's one-launch look-back over 4096-candidate chunks: a single
-    partial chunk, a chunk boundary, and more chunks (1,221) than workgroups
-    (1,024), so workgroups take a second chunk whose predecessors belong to
-    other workgroups; synthetic counts/masks against the torch reference,
-    twice in a row (the status words' epoch changes between calls)."""
+    """The pack's one-launch look-back over 16,384-candidate chunks: a single
+    partial chunk, a chunk boundary, several look-back windows (306 chunks at
+    5M), and more chunks (1,281 at 21M) than workgroups (1,024), so
+    workgroups take a second chunk whose predecessors belong to other
+    workgroups; synthetic counts/masks against the torch reference, twice in
+    a row (the status words' epoch changes between calls)."""
     import importlib
     import torch
     par = importlib.import_module(pkg.__name__ + ".parallel")
@@ -374,7 +375,7 @@ def test_pack_lookback_expiry_stays_exact(pkg, ctx):
     """A look-back wait that expires (another kernel can hold the
     CUs the earlier chunks need) must not corrupt the exchange: the chunk takes
     the slow path that counts its prefix itself.  Forced for chunk 3, and with
-    a spin limit of one iteration over 1,221 chunks: the header and every row
+    a spin limit of one iteration over 306 chunks: the header and every row
     stay exact, and mvs_pack_fallbacks counts the slow chunks."""
     import importlib
     import torch
