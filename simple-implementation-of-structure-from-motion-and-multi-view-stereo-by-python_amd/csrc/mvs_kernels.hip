@@ -1995,15 +1995,16 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // first cap rows (the receiver sees accepted > cap).  Each chunk's rows go to
 // (sum of the earlier chunks' counts) + their rank.
 // ---------------------------------------------------------------------------
-// Chunks of kAccPer x kAccThreads = 16,384 candidates, thread t of a chunk
+// Chunks of kAccPer x kAccThreads = 8,192 candidates, thread t of a chunk
 // holding candidates chunk + t + kAccThreads j (j < kAccPer): the count reads
 // stay coalesced, a workgroup has enough loads in flight to hide their
-// latency, and a 2^20 slice has 64 chunks -- one look-back window, so a
-// chunk's prefix is one round of status loads behind its predecessors' own
-// counts (4,096-candidate chunks: up to four windows walked in turn).
-constexpr int kAccThreads = 1024, kAccPer = 16, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
+// latency, and a 2^20 slice has 128 chunks (two look-back windows).  The
+// accepted candidates' mask words and points are loaded with the counts,
+// before the look-back, so that the rows go out as soon as the prefix is in.
+constexpr int kAccThreads = 1024, kAccPer = 8, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
+constexpr int kAccEpl = kAccPer * kAccWaves / 64;   // (j, wave) counts per lane of wave 0's scan
 static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the status words by MVS_ACC_CHUNK");
-static_assert(kAccPer * kAccWaves == 256, "wave 0 scans the (j, wave) counts four per lane");
+static_assert(kAccEpl == 2, "wave 0 scans the (j, wave) counts two per lane");
 
 // One launch: each chunk's rows start after every earlier chunk's accepted
 // count, found by a decoupled look-back over per-chunk status words
@@ -2058,20 +2059,27 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             c[j] = i < n ? acc_count(count, mask, ms, words, i) : 0;
         }
         uint64_t m[kAccPer], w0[kAccPer];
+        double px[kAccPer], py[kAccPer], pz[kAccPer];
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
             const bool acc = i < n && c[j] >= vlb;
             m[j] = __ballot(acc);
             w0[j] = acc ? mask[i * ms] : 0ull;
+            px[j] = py[j] = pz[j] = 0.0;
+            if (cpt && acc) {
+                px[j] = cpt[3 * i];
+                py[j] = cpt[3 * i + 1];
+                pz[j] = cpt[3 * i + 2];
+            }
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
         }
         __syncthreads();
         if (wave == 0) {
-            // exclusive scan of the 256 (j, wave) counts in index order, four
+            // exclusive scan of the 128 (j, wave) counts in index order, two
             // consecutive ones per lane
-            const int4 x4 = ((const int4*)s_cnt)[lane];
-            const int l1 = x4.x + x4.y, l2 = l1 + x4.z, tot = l2 + x4.w;
+            const int2 x2 = ((const int2*)s_cnt)[lane];
+            const int tot = x2.x + x2.y;
             int incl = tot;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
@@ -2079,7 +2087,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 if (lane >= off) incl += y;
             }
             const int ex = incl - tot;
-            ((int4*)s_cnt)[lane] = make_int4(ex, ex + x4.x, ex + l1, ex + l2);
+            ((int2*)s_cnt)[lane] = make_int2(ex, ex + x2.x);
             const uint64_t T = (uint32_t)__shfl(incl, 63, 64);   // this chunk's accepted
             // publish, then look back over the 64 chunks before b at a time
             if (lane == 0)
@@ -2170,9 +2178,9 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                     for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
                     if (cpt) {
                         // the accepted 3D point itself (binary64 bits)
-                        o[1 + words] = __double_as_longlong(cpt[3 * i]);
-                        o[2 + words] = __double_as_longlong(cpt[3 * i + 1]);
-                        o[3 + words] = __double_as_longlong(cpt[3 * i + 2]);
+                        o[1 + words] = __double_as_longlong(px[j]);
+                        o[2 + words] = __double_as_longlong(py[j]);
+                        o[3 + words] = __double_as_longlong(pz[j]);
                     }
                 }
             }

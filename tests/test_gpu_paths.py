@@ -278,7 +278,7 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     bench's exchange) and without (16-B rows) -- including a capacity below the
     accepted count (the first cap rows, the true count in the header) and an
     empty slice.  The pack's device time per call is printed (launch gaps
-    included; bound 20 us per 2^20 sweep)."""
+    included; bound 30 us per 2^20 sweep)."""
     import importlib
     import torch
     par = importlib.import_module(pkg.__name__ + ".parallel")
@@ -339,14 +339,14 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
         assert int(out[0, 0]) == acc
         # events around back-to-back launches include the inter-kernel gaps;
         # the kernel's own time is in the rocprof summaries (profiles/r04/)
-        assert us <= 20.0
+        assert us <= 30.0
 
 
-@pytest.mark.parametrize("n", [1, 16383, 16385, 5_000_001, 21_000_001])
+@pytest.mark.parametrize("n", [1, 8191, 8193, 5_000_001, 10_000_001])
 def test_pack_accepted_lookback_sizes(pkg, ctx, n):
-    """The pack's one-launch look-back over 16,384-candidate chunks: a single
-    partial chunk, a chunk boundary, several look-back windows (306 chunks at
-    5M), and more chunks (1,281 at 21M) than workgroups (1,024), so
+    """The pack's one-launch look-back over 8,192-candidate chunks: a single
+    partial chunk, a chunk boundary, several look-back windows (611 chunks at
+    5M), and more chunks (1,221 at 10M) than workgroups (1,024), so
     workgroups take a second chunk whose predecessors belong to other
     workgroups; synthetic counts/masks against the torch reference, twice in
     a row (the status words' epoch changes between calls)."""
@@ -376,7 +376,7 @@ def test_pack_lookback_expiry_stays_exact(pkg, ctx):
     """A look-back wait that expires (another kernel can hold the
     CUs the earlier chunks need) must not corrupt the exchange: the chunk takes
     the slow path that counts its prefix itself.  Forced for chunk 3, and with
-    a spin limit of one iteration over 306 chunks: the header and every row
+    a spin limit of one iteration over 611 chunks: the header and every row
     stay exact, and mvs_pack_fallbacks counts the slow chunks."""
     import importlib
     import torch
