@@ -54,7 +54,7 @@ PEAK_HBM = 8.0e12          # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
 PEAK_I8 = 5.0e15           # dense i8 MFMA ops/s (2x the 2.5 PF dense bf16; no sparsity)
 SIMDS = 1024               # 256 CUs x 4 SIMDs
 CLOCK = 2.4e9              # peak engine clock, Hz
-PMC_PATH = os.path.join(REPO, "profiles", "r03", "pmc.json")
+PMC_PATH = os.path.join(REPO, "profiles", "r04", "pmc.json")
 # kernel / score-call timing: HIP and torch events on every TIME_EVERY-th timed step
 TIME_EVERY = 5
 
@@ -117,13 +117,13 @@ def pmc_entry(scene, V, wid, n, kernel):
     return None
 
 
-def roofline(entry, V, wid, n, kms):
+def roofline(entry, V, wid, n, kms, kernel):
     """Roofs of the dominant kernel: measured HBM bytes, VALU-busy cycles and
     MFMA i8 operations per launch (PMC) over the live launch time.  The binding
     roof is the one with the largest fraction; each frac <= 1 because a unit
     cannot be busier than its peak."""
     npx = (2 * wid + 1) ** 2
-    out = {"kernel": entry["kernel"] if entry else "k_score_mma", "kernel_ms": kms,
+    out = {"kernel": entry["kernel"] if entry else kernel, "kernel_ms": kms,
            "candidates_per_launch": n, "logical_bytes_per_candidate": logical_bytes(V, wid),
            "logical_GBps": logical_bytes(V, wid) * n / (kms * 1e-3) / 1e9,
            "logical_note": "SURVEY 8(d) bytes (every candidate's V windows read once); the scorer "
@@ -415,7 +415,7 @@ def main():
         "gathered_records": gathered,
         "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream, a.thr, a.wid),
     }
-    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms)
+    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms, kernel_name)
     if solo and not a.no_overlap:
         ov = overlap_proxy(ctx, sw, V, vlb, accepted, stream, a.thr, a.wid, max(a.steps // 2, 10))
         # the same with the scorer held to 448 workgroups (224 CUs), leaving
@@ -445,7 +445,7 @@ def main():
             out["secondary"] = {"wid": a.secondary_wid, "value": n * s2 / dt2, "kernel_ms": kms2,
                                 "score_call_ms": pms2,
                                 "roofline": roofline(pmc_entry(a.scene, V, a.secondary_wid, n, kernel_name), V,
-                                                     a.secondary_wid, n, kms2)}
+                                                     a.secondary_wid, n, kms2, kernel_name)}
 
     if solo and a.scene == "dino" and not a.no_stage:
         sd = dict(np.load(os.path.join(REPO, "tests", "golden", "seeds_dino.npz")))
@@ -483,7 +483,7 @@ def main():
                           "kernel_ms": rkms, "score_call_ms": rpms,
                           "accepted_per_sweep": int((host_outputs(rsw)[1] >= 3).sum()),
                           "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"], rctx.timed_kernel()), rV, a.wid,
-                                               rsw["n"], rkms)}
+                                               rsw["n"], rkms, rctx.timed_kernel())}
         rctx.close()
 
     if solo and not a.no_cpu_baseline:

@@ -127,7 +127,7 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
 int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups, void* stream);
 int64_t mvs_pack_fallbacks(mvs_ctx* ctx);
 /* Tests only: mode > 0 sets the pack's look-back spin limit, mode < 0 sends
- * chunk -mode (8,192 candidates each) down the slow path at once, 0 restores
+ * chunk -mode (2,048 candidates each) down the slow path at once, 0 restores
  * the default. */
 int mvs_pack_debug(mvs_ctx* ctx, int64_t mode);
 /* Kernel timing (measurement only): while enabled, every enable-th scoring

@@ -325,8 +325,8 @@ struct mvs_ctx {
     int tab_mode = 0;
     int scorer_wgs = 0;   // env MVS_SCORER_WGS: k_score_tab's grid (0 = every CU, twice)
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
-    DevBuf<double> mom_w[MVS_MAX_WID + 1];     // V <= 64
-    DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V > 64
+    DevBuf<double> mom_w[MVS_MAX_WID + 1];     // 48 < V <= 64
+    DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V <= 48 or V > 64 (moments_dtab)
     bool mom_ok[MVS_MAX_WID + 1] = {};
     int moments_vp() const { return V > MVS_GROUP_VIEWS ? 64 * ((V + 63) / 64) : 16 * ((V + 15) / 16); }
     MomentsDev moments(int wid) const {
@@ -338,17 +338,19 @@ struct mvs_ctx {
         m.wid = wid;
         return m;
     }
-    // the tables of wid (10 B per (pixel, view) at V <= 64, 6 B above), built
-    // on stream s if needed; false when they do not apply (disabled, or more
-    // than 2^31 elements)
+    // the tables of wid (6 B per (pixel, view): S_b and D; 10 B at 48 < V <=
+    // 64: S_b and w), built on stream s if needed; false when they do not
+    // apply (disabled, or more than 2^31 elements).  One row of 16 pixels
+    // past the end: k_score_tab stages a tile's rows whole (16 pixels x VP),
+    // also where the last tile column runs past W
     bool ensure_moments(int wid, hipStream_t s) {
         if (tab_mode != 0) return false;
-        const int64_t elems = (int64_t)H * W * moments_vp();
+        const int64_t elems = ((int64_t)H * W + 16) * moments_vp();
         if (elems >= ((int64_t)1 << 31)) return false;
         if (!mom_ok[wid]) {
             mom_sb[wid].alloc((size_t)elems);
             HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
-            if (V > MVS_GROUP_VIEWS) {
+            if (moments_dtab(V)) {
                 mom_d[wid].alloc((size_t)elems);
                 HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
             } else {
@@ -502,7 +504,7 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.nty = (ctx->H + MVS_TILE_H - 1) / MVS_TILE_H;
         const int ntiles = t.ntx * t.nty;
         const int32_t* tiles_before = ctx->t_tiles.p;
-        ctx->t_tiles.ensure((size_t)2 * (ntiles + 4) + 8);
+        ctx->t_tiles.ensure((size_t)tc_words(ntiles));
         if (ctx->t_tiles.p != tiles_before) ctx->tiles_clean_ntiles = -1;
         const int groups = grouped ? (ctx->V + MVS_GROUP_VIEWS - 1) / MVS_GROUP_VIEWS : 1;
         // tile buckets of cap candidates (16x the mean load, at least 1024:
@@ -520,9 +522,11 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.chunk = grouped ? MVS_GROUP_CHUNK : MVS_MMA_CHUNK;
         t.groups = groups;
         t.tile_count = ctx->t_tiles.p;
-        t.fix_count = ctx->t_tiles.p + ntiles + 1;
-        t.n_items = ctx->t_tiles.p + ntiles + 2;
-        t.done = ctx->t_tiles.p + ntiles + 3;
+        int32_t* ctl = ctx->t_tiles.p + (int64_t)ntiles * kTcStride;   // one 128-B line per counter
+        t.head = ctl;
+        t.fix_count = ctl + 32;
+        t.n_items = ctl + 64;
+        t.done = ctl + 96;
         t.sorted = (int2*)ctx->t_cand.p;
         t.fix_list = (int4*)(ctx->t_cand.p + 2 * (size_t)ntiles * cap);
         // at most one partial chunk per tile beyond the full ones

@@ -59,8 +59,12 @@ struct ScoreArgs {
 };
 
 // Scratch of the tiled scorer (device pointers, sized by the host).
-//   tile_count[ntiles+12]: per-tile counts, then the queue head, fix_count,
-//   n_items, done (k_score_fix's finishing ticket), 8 per-XCD queue heads
+//   tile_count[k * MVS_TC_STRIDE]: tile k's count (stride 1: a wave's atomics
+//   on 64 neighbouring tiles share two cache lines -- measured 20 us faster
+//   per 2^20 sweep in k_bin than one line per tile, stride 32); then the
+//   control block, one 128-B line per counter (their atomics never queue
+//   behind each other's): the queue head, fix_count, n_items, done
+//   (k_score_fix's finishing ticket) -- tc_words(ntiles) ints
 //   sorted[ntiles*cap] = {id, pk} per tile bucket (k_bin writes candidate
 //   rank r of tile k at k*cap + r), pk = (x - x0) | (y - y0) << 4 | R << 7
 //   (pixel inside the tile); a candidate of rank >= cap overflows to fix_list
@@ -70,12 +74,24 @@ struct ScoreArgs {
 //   scores by the direct path -- bucket overflow (k_bin) and candidates with
 //   a view decision inside the guard band (the tiled scorers, numpy-order
 //   ctNcc there)
+#ifndef MVS_TC_STRIDE
+#define MVS_TC_STRIDE 1
+#endif
+constexpr int kTcStride = MVS_TC_STRIDE;
+inline int64_t tc_words(int ntiles) { return (int64_t)ntiles * kTcStride + 4 * 32; }
+
+// The per-scene moment tables hold D = n S_bb - S_b^2 (int32) where the
+// scorer stages them in LDS (V <= 48: k_score_tab's tile rows; V > 64:
+// k_score_mma_v) and w = 1/sqrt(D) (binary64) for 48 < V <= 64.
+inline bool moments_dtab(int V) { return V <= 48 || V > 64; }
+
 struct TiledArgs {
     int ntx, nty, ntiles;
     int tw, th;                // tile size in pixels (x, y): 16 x 8
     int chunk;                 // candidates per work item
     int cap;                   // bucket capacity per tile (candidates)
-    int32_t* tile_count;
+    int32_t* tile_count;       // tile k's count at k * kTcStride
+    int32_t* head;             // the scorers' work-queue head
     int2* sorted;
     int4* fix_list;
     int32_t* fix_count;
@@ -99,15 +115,19 @@ struct TiledArgs {
 // with a valid window and view v, element (y * W + x) * VP + v holds
 // S_b = the sum of the signed bytes s = g - 128 over the (2 wid + 1)^2 window
 // (int16: |S_b| <= 121 * 128) and
-//   V <= 64 (k_score_tab): w = 1 / sqrt(n S_bb - S_b^2) (v_rsq_f64 + one
-//     Newton step; nan for a constant window and for the pad views
-//     V <= v < VP), VP = 16 ceil(V / 16);
-//   V > 64 (k_score_mma_v): D = n S_bb - S_b^2 (int32, exact; -1 for the pad
-//     views), VP = 64 ceil(V / 64).
+//   48 < V <= 64 (k_score_tab, global table reads): w = 1 / sqrt(n S_bb -
+//     S_b^2) (v_rsq_f64 + one Newton step; nan for a constant window and for
+//     the pad views V <= v < VP), VP = 64;
+//   V <= 48 (k_score_tab, the tile's rows staged in LDS) and V > 64
+//     (k_score_mma_v): D = n S_bb - S_b^2 (int32, exact; -1 for the pad
+//     views; the scorer forms w from D with the same two instructions),
+//     VP = 16 ceil(V / 16) resp. 64 ceil(V / 64).
+// The tables hold H W + 16 pixels (a tile row staged whole may run 16 pixels
+// past the last one).
 struct MomentsDev {
     int16_t* sb;
-    double* w;      // V <= 64
-    int32_t* d;     // V > 64
+    double* w;      // 48 < V <= 64
+    int32_t* d;     // moments_dtab(V): V <= 48 or V > 64
     int VP;
     int wid;
 };
@@ -149,7 +169,7 @@ struct ExpandArgs {
 #define MVS_MMA_CHUNK 1024    // candidates per work item, V <= 64 (whole tiles, as a rule)
 #define MVS_GROUP_VIEWS 64    // views per group when V > 64
 #define MVS_GROUP_CHUNK 116   // candidates per work item when V > 64 (their reference rows staged)
-#define MVS_ACC_CHUNK 8192    // candidates per chunk of the exchange's pack (k_acc_pack)
+#define MVS_ACC_CHUNK 2048    // candidates per chunk of the exchange's pack (k_acc_pack)
 
 extern "C" {
 // RGB -> stack and gv (one pass, coalesced on both sides); the caller zeroes

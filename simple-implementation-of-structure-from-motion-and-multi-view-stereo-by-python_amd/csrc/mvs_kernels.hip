@@ -346,7 +346,17 @@ __device__ unsigned long long g_stamps[4096 * 16];
 constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
 constexpr int kMmaGrid = 256;         // the scorers' workgroups: one per CU; the queue balances
 
-// items opened by ranks [base, base + c) of a tile: chunk j starts at j chunk
+// the number of work items ranks [base, base + c) of a tile open: chunk j
+// (bucket entries [j chunk, (j+1) chunk), below cap) opens with rank j chunk
+DEV int items_opened(const TiledArgs& t, int base, int c) {
+    if (c <= 0) return 0;
+    const int lo = (base + t.chunk - 1) / t.chunk;
+    const int hi = (min(base + c, t.cap) + t.chunk - 1) / t.chunk;
+    return max(hi - lo, 0);
+}
+
+// items opened by ranks [base, base + c) of a tile (one atomic each: the
+// global-histogram path of very large images)
 DEV void open_items(const TiledArgs& t, int tile, int base, int c) {
     for (int j = (base + t.chunk - 1) / t.chunk; j * t.chunk < base + c && j * t.chunk < t.cap; ++j)
         t.items[atomicAdd(t.n_items, 1)] = make_int4(tile, j, 0, 0);
@@ -360,6 +370,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     // candidate reads its reference camera's 16 values there instead of by
     // per-lane global loads
     __shared__ double s_cam[MVS_MAX_VIEWS][16];
+    __shared__ int s_open[kBinBlock / 64 + 1];
     const int words = (sc.V + 63) >> 6;
     for (int k = threadIdx.x; k < sc.V * 16; k += blockDim.x) {
         const int v = k >> 4, f = k & 15;
@@ -410,7 +421,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         if (LDSHIST) {
             lr[k] = atomicAdd(&hist[tile], 1);
         } else {
-            lr[k] = atomicAdd(&t.tile_count[tile], 1);
+            lr[k] = atomicAdd(&t.tile_count[tile * kTcStride], 1);
             open_items(t, tile, lr[k], 1);
         }
     }
@@ -424,14 +435,39 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
             const int b = threadIdx.x + j * kBinBlock;
             const int c = b < t.ntiles ? hist[b] : 0;
-            bs[j] = c ? atomicAdd(&t.tile_count[b], c) : 0;
+            bs[j] = c ? atomicAdd(&t.tile_count[b * kTcStride], c) : 0;
         }
+        // the work items this workgroup opens (chunk starts j chunk inside a
+        // returned rank range), appended with ONE n_items atomic per
+        // workgroup: slot = its base + the thread's exclusive prefix
+        int nopen = 0;
+#pragma unroll
+        for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
+            const int b = threadIdx.x + j * kBinBlock;
+            if (b < t.ntiles) nopen += items_opened(t, bs[j], hist[b]);
+        }
+        int incl = nopen;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int o = __shfl_up(incl, d, 64);
+            if ((threadIdx.x & 63) >= d) incl += o;
+        }
+        if ((threadIdx.x & 63) == 63) s_open[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int run = 0;
+            for (int w = 0; w < kBinBlock / 64; ++w) { const int c = s_open[w]; s_open[w] = run; run += c; }
+            s_open[kBinBlock / 64] = run ? atomicAdd(t.n_items, run) : 0;
+        }
+        __syncthreads();
+        int slot = s_open[kBinBlock / 64] + s_open[threadIdx.x >> 6] + incl - nopen;
 #pragma unroll
         for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
             const int b = threadIdx.x + j * kBinBlock;
             if (b < t.ntiles) {
                 const int c = hist[b];
-                if (c) open_items(t, b, bs[j], c);
+                for (int q = (bs[j] + t.chunk - 1) / t.chunk; c && q * t.chunk < bs[j] + c && q * t.chunk < t.cap; ++q)
+                    t.items[slot++] = make_int4(b, q, 0, 0);
                 hist[b] = bs[j];
             }
         }
@@ -618,7 +654,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
     const int n_units = *t.n_items;
-    int32_t* head = &t.tile_count[t.ntiles];
+    int32_t* head = t.head;
 
     // The region of an item (gv rows, signed bytes) goes to LDS by LDS-DMA
     // (global_load_lds_dwordx4: 64 lanes x 16 B land contiguously), 32 B per
@@ -1313,7 +1349,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
     const int n_items = *t.n_items;
-    int32_t* head = &t.tile_count[t.ntiles];
+    int32_t* head = t.head;
 
     // region piece k (view k / 2RPV, row, half) of view group g at a tile: its
     // gv address; rows outside the image are clamped (their pixels are never
@@ -1770,7 +1806,7 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
     const int nfix = *t.fix_count;
     const int active = nfix > kFixSmall ? (int)gridDim.x : kFixBase;   // uniform over the grid
     if ((int)blockIdx.x >= active) return;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += active * 256) t.tile_count[k] = 0;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += active * 256) t.tile_count[k * kTcStride] = 0;
     for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
          k += active * 4) {
         const int4 f = t.fix_list[k];
@@ -1786,8 +1822,7 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
     if (threadIdx.x == 0 && atomicAdd(t.done, 1) == active - 1) {
         *t.fix_count = 0;
         *t.n_items = 0;
-        t.tile_count[t.ntiles] = 0;   // the queue head
-        for (int l = 0; l < 8; ++l) t.tile_count[t.ntiles + 4 + l] = 0;   // the per-XCD heads (MVS_XCD_QUEUE)
+        *t.head = 0;
         *t.done = 0;
     }
 }
@@ -1995,16 +2030,19 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // first cap rows (the receiver sees accepted > cap).  Each chunk's rows go to
 // (sum of the earlier chunks' counts) + their rank.
 // ---------------------------------------------------------------------------
-// Chunks of kAccPer x kAccThreads = 8,192 candidates, thread t of a chunk
-// holding candidates chunk + t + kAccThreads j (j < kAccPer): the count reads
-// stay coalesced, a workgroup has enough loads in flight to hide their
-// latency, and a 2^20 slice has 128 chunks (two look-back windows).  The
-// accepted candidates' mask words and points are loaded with the counts,
-// before the look-back, so that the rows go out as soon as the prefix is in.
-constexpr int kAccThreads = 1024, kAccPer = 8, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
-constexpr int kAccEpl = kAccPer * kAccWaves / 64;   // (j, wave) counts per lane of wave 0's scan
+// Chunks of kAccPer x kAccThreads = 2,048 candidates, thread t of a chunk
+// holding candidates chunk + t + kAccThreads j (j < kAccPer): the reads stay
+// coalesced, a 2^20 slice has 512 chunks (two workgroups on every CU), and
+// the look-back walks at most a few 64-chunk windows.  Each candidate's first
+// mask word is loaded with its count (records: the count IS its popcount), the
+// accepted candidates' points as soon as the counts are in; they stay in
+// flight across the chunk's scan and look-back (LDS-only barriers), so that
+// the rows go out as soon as the prefix is in.
+constexpr int kAccThreads = 256, kAccPer = 8, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
+constexpr int kAccE = kAccPer * kAccWaves;          // (j, wave) counts of a chunk
+constexpr int kAccEpl = (kAccE + 63) / 64;          // of them per lane of wave 0's scan
 static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the status words by MVS_ACC_CHUNK");
-static_assert(kAccEpl == 2, "wave 0 scans the (j, wave) counts two per lane");
+static_assert(kAccE <= 128, "wave 0 scans at most two (j, wave) counts per lane");
 
 // One launch: each chunk's rows start after every earlier chunk's accepted
 // count, found by a decoupled look-back over per-chunk status words
@@ -2020,7 +2058,7 @@ static_assert(kAccEpl == 2, "wave 0 scans the (j, wave) counts two per lane");
 // agent-scope atomics: a word carries all a reader needs, and a release or
 // acquire would write back or invalidate this XCD's L2 at every step.
 // debug (tests only): > 0 = the spin limit; < 0 = chunk -debug falls back at once.
-constexpr int kAccGrid = 1024;
+constexpr int kAccGrid = 2048;
 constexpr uint32_t kAccSpin = 1u << 22;
 
 DEV int acc_count(const int32_t* __restrict__ count, const uint64_t* __restrict__ mask, int64_t ms, int words,
@@ -2050,22 +2088,30 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
     const uint64_t E = epoch << 34;
     const uint32_t spin_limit = debug > 0 ? (uint32_t)debug : kAccSpin;
     for (int64_t b = blockIdx.x; b < nch; b += gridDim.x) {
-        // every load of the chunk in flight at once: the counts, then the
-        // accepted candidates' first mask words
+        // every load of the chunk in flight at once: the first mask words and
+        // the counts (records: popcounts of the words)
+        uint64_t m[kAccPer], w0[kAccPer];
         int c[kAccPer];
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            c[j] = i < n ? acc_count(count, mask, ms, words, i) : 0;
+            w0[j] = i < n ? mask[i * ms] : 0ull;
+            c[j] = i < n && count ? count[i] : 0;
         }
-        uint64_t m[kAccPer], w0[kAccPer];
+#pragma unroll
+        for (int j = 0; j < kAccPer; ++j) {
+            const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+            if (i < n && !count) {
+                c[j] = __popcll(w0[j]);
+                for (int q = 1; q < words; ++q) c[j] += __popcll(mask[i * ms + q]);
+            }
+        }
         double px[kAccPer], py[kAccPer], pz[kAccPer];
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
             const bool acc = i < n && c[j] >= vlb;
             m[j] = __ballot(acc);
-            w0[j] = acc ? mask[i * ms] : 0ull;
             px[j] = py[j] = pz[j] = 0.0;
             if (cpt && acc) {
                 px[j] = cpt[3 * i];
@@ -2074,20 +2120,30 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             }
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
         }
-        __syncthreads();
+        lds_barrier();   // the points stay in flight
         if (wave == 0) {
-            // exclusive scan of the 128 (j, wave) counts in index order, two
+            // exclusive scan of the (j, wave) counts in index order, kAccEpl
             // consecutive ones per lane
-            const int2 x2 = ((const int2*)s_cnt)[lane];
-            const int tot = x2.x + x2.y;
+            int x[kAccEpl], tot = 0;
+#pragma unroll
+            for (int q = 0; q < kAccEpl; ++q) {
+                const int e = lane * kAccEpl + q;
+                x[q] = e < kAccE ? s_cnt[e] : 0;
+                tot += x[q];
+            }
             int incl = tot;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
                 const int y = __shfl_up(incl, off, 64);
                 if (lane >= off) incl += y;
             }
-            const int ex = incl - tot;
-            ((int2*)s_cnt)[lane] = make_int2(ex, ex + x2.x);
+            int ex = incl - tot;
+#pragma unroll
+            for (int q = 0; q < kAccEpl; ++q) {
+                const int e = lane * kAccEpl + q;
+                if (e < kAccE) s_cnt[e] = ex;
+                ex += x[q];
+            }
             const uint64_t T = (uint32_t)__shfl(incl, 63, 64);   // this chunk's accepted
             // publish, then look back over the 64 chunks before b at a time
             if (lane == 0)
@@ -2136,7 +2192,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 s_total = (int64_t)T;
             }
         }
-        __syncthreads();
+        lds_barrier();
         if (s_slow) {
             // the slow path: the accepted candidates of [0, b chunk) counted
             // from the inputs by the whole workgroup (no other workgroup involved)
@@ -2185,7 +2241,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();   // s_cnt is rewritten by the next chunk
     }
 }
 
@@ -2370,10 +2426,10 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         t->chunk != (grouped ? kGroupChunk : kMmaChunk) || t->groups != (grouped ? (sc->V + 63) / 64 : 1) ||
         sc->V > MVS_MAX_VIEWS)
         return -3;
-    // tile counters, the work-queue head (tile_count[ntiles]) and fix_count:
-    // left at zero by the previous batch's item scan unless zero_first
+    // tile counters and the control block (queue head, fix_count, n_items,
+    // done): left at zero by the previous batch's k_score_fix unless zero_first
     if (t->zero_first &&
-        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * (t->ntiles + 12), s) != hipSuccess)
+        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * tc_words(t->ntiles), s) != hipSuccess)
         return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);

@@ -113,7 +113,7 @@ DEV void static_for(F&& f) {
 // (uniform: scalar loads)
 DEV int4 item_desc(const TiledArgs& t, const int4* __restrict__ items, int v) {
     const int4 it = items[v];
-    const int cnt = min(t.tile_count[it.x], t.cap);
+    const int cnt = min(t.tile_count[it.x * kTcStride], t.cap);
     return make_int4(it.x, it.x * t.cap + it.y * t.chunk, min(cnt - it.y * t.chunk, t.chunk), 0);
 }
 

@@ -173,9 +173,22 @@ struct TabGeom {
     static constexpr int RB = VP * MmaGeom<WID>::VS;    // one region buffer (+16 zero bytes)
     static constexpr int CB = kTabChunk * 8;            // one candidate buffer
     static constexpr int FIXED = kTabWaves * 32 * (int)sizeof(TabInfo) + 65 * 8 + 64;
-    // two buffers of each where two workgroups per CU still fit (80 KiB each)
-    static constexpr bool DB = 2 * (RB + 16) + 2 * CB + FIXED <= 80 * 1024 - 512;
+    // LT: the tile's table rows (S_b int16, D int32 of 8 rows x 16 pixels x
+    // VP views) staged in LDS next to one region and list buffer, where two
+    // workgroups per CU still fit (80 KiB each): V <= 48 at every WID
+    static constexpr int TS = 8 * 16 * VP * 2, TD = 8 * 16 * VP * 4;
+    static constexpr bool LT = (RB + 16) + CB + TS + TD + FIXED <= 80 * 1024 - 512;
+    // else two buffers of region and list where they fit (global table reads)
+    static constexpr bool DB = !LT && 2 * (RB + 16) + 2 * CB + FIXED <= 80 * 1024 - 512;
 };
+
+// w = 1/sqrt(D): the two instructions k_moments uses for its w table (bit
+// for bit the same value)
+DEV double w_of(int db) {
+    const double D = (double)db;
+    const double w = __builtin_amdgcn_rsq(D);
+    return w * (1.5 - 0.5 * D * w * w);
+}
 
 template <int WID, int NBLK, bool FAST>
 __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
@@ -185,7 +198,8 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     using TG = TabGeom<WID, NBLK>;
     constexpr int NB = G::NB, NPX = G::NPX, KS = G::KS, VS = G::VS, C0 = G::C0;
     constexpr int VP = TG::VP;
-    constexpr bool DB = TG::DB;
+    constexpr bool DB = TG::DB, LT = TG::LT;
+    static_assert(LT == (NBLK <= 3), "the host builds D tables (moments_dtab) exactly for V <= 48");
     constexpr int RPV = VS / 32;                                          // region rows per view incl. the pad row
     constexpr int PF = (VP * RPV * 2 + kTabThreads - 1) / kTabThreads;    // 16-B pieces per thread
     constexpr int RB = TG::RB, CB = TG::CB;
@@ -195,6 +209,9 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB + 16], s_reg1[DB ? RB + 16 : 16];
     __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[DB ? CB : 16];
     __shared__ __attribute__((aligned(16))) TabInfo s_ti[kTabWaves * 32];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tab[LT ? TG::TS + TG::TD : 16];   // LT: [S_b rows][D rows]
+    const int16_t* ls_sb = (const int16_t*)s_tab;
+    const int32_t* ls_d = (const int32_t*)(s_tab + (LT ? TG::TS : 0));
     __shared__ int s_ids[2];
     __shared__ double s_recip[65];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -209,7 +226,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
     const int n_units = *t.n_items;
-    int32_t* head = &t.tile_count[t.ntiles];
+    int32_t* head = t.head;
     const int16_t* __restrict__ tsb = mt.sb;
     const double* __restrict__ tw = mt.w;
 
@@ -222,7 +239,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
         uint8_t* base = region_buf(bufc);
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
-            const int k = tid + p * kTabThreads;
+            const int k = opaque(tid) + p * kTabThreads;   // recomputed per piece: no long-lived offsets
             if (k < npiece) {
                 const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
                 const int y = min(max(yr0 + (r2 >> 1), 0), sc.H - 1);
@@ -232,42 +249,62 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                                                  16, 0, 0);
             }
         }
+        if constexpr (LT) {
+            // the tile's 8 rows of 16 pixels x VP views, S_b then D: each row
+            // one contiguous run of the tables (rows past H clamped; their
+            // pixels hold no candidate)
+            constexpr int PS = 2 * VP, PD = 4 * VP, NPT = 8 * (PS + PD);   // 16-B pieces
+            const int yt0 = ty * MVS_TILE_H;
+#pragma unroll
+            for (int p = 0; p < (NPT + kTabThreads - 1) / kTabThreads; ++p) {
+                const int k = opaque(tid) + p * kTabThreads;
+                if (k < NPT) {
+                    const uint8_t* src;
+                    if (k < 8 * PS) {
+                        const int r = k / PS, c = k - r * PS;
+                        const int64_t px = (int64_t)min(yt0 + r, sc.H - 1) * sc.W + x0;
+                        src = (const uint8_t*)(mt.sb + px * VP) + 16 * c;
+                    } else {
+                        const int k2 = k - 8 * PS, r = k2 / PD, c = k2 - r * PD;
+                        const int64_t px = (int64_t)min(yt0 + r, sc.H - 1) * sc.W + x0;
+                        src = (const uint8_t*)(mt.d + px * VP) + 16 * c;
+                    }
+                    __builtin_amdgcn_global_load_lds((const void*)src,
+                                                     (void __attribute__((address_space(3)))*)(s_tab + (p * kTabThreads + wave * 64) * 16),
+                                                     16, 0, 0);
+                }
+            }
+        }
         uint8_t* cbase = cand_buf(bufc);
         const int32_t* csrc = (const int32_t*)(sorted + d.y);
 #pragma unroll
         for (int p = 0; p < 2 * kTabChunk / kTabThreads; ++p) {
             const int k = tid + p * kTabThreads;
-            if (k < 2 * d.z)
+            if (k < 2 * d.w)
                 __builtin_amdgcn_global_load_lds((const void*)(csrc + k),
                                                  (void __attribute__((address_space(3)))*)(cbase + (p * kTabThreads + wave * 64) * 4),
                                                  4, 0, 0);
         }
     };
 
-#ifdef MVS_XCD_QUEUE
-    // XCD-aware queue (A/B switch): the item list in 8 contiguous ranges, one
-    // per workgroup label blockIdx % 8 (workgroups b and b + 8 share an XCD as
-    // dispatched, so a range's tiles -- and their overlapping regions -- meet
-    // in one L2); a label's workgroups take its range first, then the others'
-    // (thread 0 remembers the exhausted ranges); placement changes only speed
-    int32_t* heads = &t.tile_count[t.ntiles + 4];
-    uint32_t dead = 0;
-    auto claim = [&]() -> int {
-        for (int k = 0; k < 8; ++k) {
-            const int l = (blockIdx.x + k) & 7;
-            if ((dead >> l) & 1u) continue;
-            const int b = (int)((int64_t)n_units * l / 8), e = (int)((int64_t)n_units * (l + 1) / 8);
-            const int v = b < e ? atomicAdd(&heads[l], 1) : e;
-            if (b + v < e) return b + v;
-            dead |= 1u << l;
-        }
-        return n_units;
-    };
-#else
     auto claim = [&]() -> int { return atomicAdd(head, 1); };
-#endif
+    // an item's descriptor (tile, first bucket entry, count, entries staged):
+    // the list is staged as a whole chunk (bounded by the bucket), so that its
+    // LDS-DMA needs no count -- the count arrives a round later
+    auto desc = [&](int2 it, int cnt) -> int4 {
+        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y);
+        const int c = __builtin_amdgcn_readfirstlane(cnt);
+        return make_int4(tile, tile * t.cap + j * t.chunk, min(min(c, t.cap) - j * t.chunk, t.chunk),
+                         min(t.chunk, t.cap - j * t.chunk));
+    };
+    // vector loads (a lane-dependent-looking address): their wait is the
+    // in-order vmcnt at the round's end, not lgkmcnt(0) in front of every LDS
+    // read of the round
+    auto item_v = [&](int v) -> int2 { return *(const int2*)(items + opaque(v)); };
+    auto count_v = [&](int tile) -> int { return t.tile_count[opaque(tile * kTcStride)]; };
     // the item pipeline: while item k is scored, item k+1's region and list
-    // (DB), item k+2's descriptor and thread 0's claim of item k+3 are in flight
+    // (DB) and its tile's count, item k+2's (tile, chunk) and thread 0's claim
+    // of item k+3 are in flight
     if (tid == 0) {
         s_ids[0] = claim();
         s_ids[1] = claim();
@@ -276,11 +313,14 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
     int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
     if (cur >= n_units) return;
-    int4 dcur = item_desc(t, items, cur);
-    dcur = make_int4(__builtin_amdgcn_readfirstlane(dcur.x), __builtin_amdgcn_readfirstlane(dcur.y),
-                     __builtin_amdgcn_readfirstlane(dcur.z), 0);
+    int4 dcur;
+    {
+        const int2 it = item_v(cur);
+        dcur = desc(it, count_v(it.x));
+    }
     stage(dcur, std::integral_constant<int, 0>{});
-    int4 dnx1 = nx1 < n_units ? item_desc(t, items, nx1) : make_int4(0, 0, 0, 0);
+    int2 it1 = nx1 < n_units ? item_v(nx1) : make_int2(0, 0);
+    it1 = make_int2(__builtin_amdgcn_readfirstlane(it1.x), __builtin_amdgcn_readfirstlane(it1.y));
     int pend = 0;
     if (tid == 0) pend = claim();
     __syncthreads();   // everyone has read s_ids before they are rewritten
@@ -294,19 +334,22 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
         // ---- 1. this item's region and list have landed (every wave's DMA) ----
         TSTAMP(ts0);
         if (tid == 0) s_ids[0] = pend;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's LDS-DMA, before the barrier
         __syncthreads();
         TSTAMP(ts1);
         const int nx2 = __builtin_amdgcn_readfirstlane(s_ids[0]);
-        // the next item's region and list into the other buffer, the descriptor
-        // after it, thread 0's claim of the one after that
+        // item k+2's (tile, chunk) and item k+1's count (consumed at the
+        // round's end), item k+1's region and list into the other buffer,
+        // thread 0's claim of the one after that
+        const int4 dst1 = make_int4(it1.x, it1.x * t.cap + it1.y * t.chunk, 0, min(t.chunk, t.cap - it1.y * t.chunk));
         if constexpr (DB) {
-            if (nx1 < n_units) stage(dnx1, std::integral_constant<int, buf ^ 1>{});
+            if (nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
         }
-        int4 dnx2 = make_int4(0, 0, 0, 0);
-        if (nx2 < n_units) {
-            dnx2 = item_desc(t, items, nx2);
-            if (tid == 0) pend = claim();
-        }
+        // unconditional (clamped) loads: no branch, no register reset that
+        // would wait for the LDS-DMA just issued
+        const int2 it2 = item_v(min(nx2, n_units - 1));
+        const int c1 = count_v(it1.x);
+        if (nx2 < n_units && tid == 0) pend = claim();
         const int ty = dcur.x / t.ntx, tx = dcur.x - ty * t.ntx;
         const int tix0 = ((ty * MVS_TILE_H) * sc.W + tx * MVS_TILE_W) * VP;   // table element of the tile origin
         // ---- 2. this wave's M-blocks, sorted by row pair inside the wave ----
@@ -361,11 +404,17 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                 if (kh == 0) {
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
-                        const int tix = tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
+                        // LT: element of the pixel inside the staged tile rows
+                        const int tix = LT ? (rrel[h] * MVS_TILE_W + qrel[h]) * VP : tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
                         ti[16 * h + m].tix = tix;
                         ti[16 * h + m].R = valid[h] ? Rv[h] : -1;
-                        sa_raw[h] = tsb[tix + Rv[h]];
-                        wa_raw[h] = tw[tix + Rv[h]];
+                        if constexpr (LT) {
+                            sa_raw[h] = ls_sb[tix + Rv[h]];
+                            wa_raw[h] = w_of(ls_d[tix + Rv[h]]);
+                        } else {
+                            sa_raw[h] = tsb[tix + Rv[h]];
+                            wa_raw[h] = tw[tix + Rv[h]];
+                        }
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -381,8 +430,13 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                         const int tix = ti[16 * h + 4 * kh + i].tix + m;
 #pragma unroll
                         for (int nb = 0; nb < NBLK; ++nb) {
-                            sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
-                            wv[i & 1][h][nb] = tw[tix + 16 * nb];
+                            if constexpr (LT) {
+                                sbv[i & 1][h][nb] = ls_sb[tix + 16 * nb];
+                                wv[i & 1][h][nb] = w_of(ls_d[tix + 16 * nb]);
+                            } else {
+                                sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
+                                wv[i & 1][h][nb] = tw[tix + 16 * nb];
+                            }
                         }
                     }
                 };
@@ -508,7 +562,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                         const TabInfo c = ti[16 * h + 4 * kh + i];
                         const float gT = 2e-6f * fabsf(c.T);
                         double ca = 0.0;
-                        if constexpr (!FAST) ca = c.R < 0 ? 0.0 : kn * tw[c.tix + c.R];
+                        if constexpr (!FAST) ca = c.R < 0 ? 0.0 : kn * (LT ? w_of(ls_d[c.tix + c.R]) : tw[c.tix + c.R]);
                         double sa = 0.0;
                         uint64_t g = 0;
                         float ax[NBLK];
@@ -613,12 +667,12 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
         if constexpr (!DB) {
             // one buffer: every wave is done with it before the next item lands
             __syncthreads();
-            stage(dnx1, std::integral_constant<int, 0>{});
+            stage(dst1, std::integral_constant<int, 0>{});
         }
         cur = nx1;
-        dcur = dnx1;
+        dcur = desc(it1, c1);
         nx1 = nx2;
-        dnx1 = dnx2;
+        it1 = make_int2(__builtin_amdgcn_readfirstlane(it2.x), __builtin_amdgcn_readfirstlane(it2.y));
         return true;
     };
     for (;;) {
@@ -659,8 +713,8 @@ extern "C" int mvs_read_stamps_tab(unsigned long long* out) {
 #endif
 
 extern "C" int mvs_launch_moments(const SceneDev* sc, const MomentsDev* mt, hipStream_t s) {
-    const bool dtab = sc->V > 64;
-    if (mt->VP != (dtab ? 64 * ((sc->V + 63) / 64) : 16 * ((sc->V + 15) / 16))) return -3;
+    const bool dtab = moments_dtab(sc->V);
+    if (mt->VP != (sc->V > 64 ? 64 * ((sc->V + 63) / 64) : 16 * ((sc->V + 15) / 16))) return -3;
     const dim3 grid((unsigned)((sc->W + kMomW - 1) / kMomW), (unsigned)((sc->H + kMomH - 1) / kMomH),
                     (unsigned)(mt->VP / kMomV));
 #define MVS_MOM(W_) (dtab ? (const void*)k_moments<W_, true> : (const void*)k_moments<W_, false>)

@@ -342,11 +342,11 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
         assert us <= 30.0
 
 
-@pytest.mark.parametrize("n", [1, 8191, 8193, 5_000_001, 10_000_001])
+@pytest.mark.parametrize("n", [1, 2047, 2049, 200_001, 5_000_001])
 def test_pack_accepted_lookback_sizes(pkg, ctx, n):
-    """The pack's one-launch look-back over 8,192-candidate chunks: a single
-    partial chunk, a chunk boundary, several look-back windows (611 chunks at
-    5M), and more chunks (1,221 at 10M) than workgroups (1,024), so
+    """The pack's one-launch look-back over 2,048-candidate chunks: a single
+    partial chunk, a chunk boundary, several look-back windows (98 chunks at
+    200k), and more chunks (2,442 at 5M) than workgroups (2,048), so
     workgroups take a second chunk whose predecessors belong to other
     workgroups; synthetic counts/masks against the torch reference, twice in
     a row (the status words' epoch changes between calls)."""
@@ -376,12 +376,12 @@ def test_pack_lookback_expiry_stays_exact(pkg, ctx):
     """A look-back wait that expires (another kernel can hold the
     CUs the earlier chunks need) must not corrupt the exchange: the chunk takes
     the slow path that counts its prefix itself.  Forced for chunk 3, and with
-    a spin limit of one iteration over 611 chunks: the header and every row
+    a spin limit of one iteration over 489 chunks: the header and every row
     stay exact, and mvs_pack_fallbacks counts the slow chunks."""
     import importlib
     import torch
     par = importlib.import_module(pkg.__name__ + ".parallel")
-    n = 5_000_001
+    n = 1_000_001
     g = torch.Generator().manual_seed(3)
     count = torch.randint(0, 8, (n,), generator=g, dtype=torch.int32)
     mask = torch.randint(-2**62, 2**62, (n, 1), generator=g, dtype=torch.int64)
