@@ -182,8 +182,21 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
     e1.synchronize()
     if int(out[0, 0].item()) != accepted:
         raise RuntimeError(f"pack header {int(out[0, 0].item())} != {accepted} accepted")
+    # the same pack without the points: 16-B rows [index, mask word]
+    out16 = torch.empty((cap + 1, par.points_width(words, points=False)), dtype=torch.int64, device=sw["c"].device)
+    for _ in range(10):
+        score(ctx, sw, wid, thr, stream)
+    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e2.record(stream)
+    for _ in range(20):
+        ctx.pack_accepted(sw["off"], pc, pm, vlb, out16, stream=stream.cuda_stream)
+    e3.record(stream)
+    e3.synchronize()
+    if int(out16[0, 0].item()) != accepted:
+        raise RuntimeError(f"16-B pack header {int(out16[0, 0].item())} != {accepted} accepted")
     return {"row_bytes": row, "rows_per_rank": accepted, "bytes_per_rank": row * (cap + 1),
             "pack_us": e0.elapsed_time(e1) / 20 * 1e3,
+            "pack_us_16B_rows": e2.elapsed_time(e3) / 20 * 1e3,
             "received_per_rank_at_n8_MB": 7 * row * (cap + 1) / 1e6,
             "note": "rows [global index, mask word, x, y, z]: the accepted 3D points themselves; "
                     "pack = mvs_pack_accepted (count + ballot-compacted rows, no host sync), device time "

@@ -525,12 +525,14 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         int32_t* ctl = ctx->t_tiles.p + (int64_t)ntiles * kTcStride;   // one 128-B line per counter
         t.head = ctl;
         t.fix_count = ctl + 32;
-        t.n_items = ctl + 64;
-        t.done = ctl + 96;
+        t.done = ctl + 64;
+        t.n_items = ctl + 96;
         t.sorted = (int2*)ctx->t_cand.p;
         t.fix_list = (int4*)(ctx->t_cand.p + 2 * (size_t)ntiles * cap);
-        // at most one partial chunk per tile beyond the full ones
-        ctx->t_items.ensure((size_t)(n / std::max(t.chunk, 1) + ntiles + 2));
+        // at most one partial chunk per tile beyond the full ones, in any one
+        // of the kItemSegs segments
+        t.item_seg = (int)(n / std::max(t.chunk, 1) + ntiles + 2);
+        ctx->t_items.ensure((size_t)kItemSegs * t.item_seg);
         t.items = ctx->t_items.p;
         t.zero_first = ctx->tiles_clean_ntiles != ntiles ? 1 : 0;
         t.grid = ctx->scorer_wgs;

@@ -68,8 +68,9 @@ struct ScoreArgs {
 //   sorted[ntiles*cap] = {id, pk} per tile bucket (k_bin writes candidate
 //   rank r of tile k at k*cap + r), pk = (x - x0) | (y - y0) << 4 | R << 7
 //   (pixel inside the tile); a candidate of rank >= cap overflows to fix_list
-//   items[n_items] = (tile, chunk j, 0, 0): bucket entries [j chunk, (j+1)
-//   chunk) of the tile, appended by k_bin in the order the chunks were opened
+//   items = (tile, chunk j, 0, 0): bucket entries [j chunk, (j+1) chunk) of
+//   the tile, appended by k_bin in the order the chunks were opened, to
+//   segment b % kItemSegs of the opening workgroup b (ItemMap: one list)
 //   fix_list[n], fix_count: {id, tile, pk, 0} of the candidates k_score_fix
 //   scores by the direct path -- bucket overflow (k_bin) and candidates with
 //   a view decision inside the guard band (the tiled scorers, numpy-order
@@ -78,12 +79,20 @@ struct ScoreArgs {
 #define MVS_TC_STRIDE 1
 #endif
 constexpr int kTcStride = MVS_TC_STRIDE;
-inline int64_t tc_words(int ntiles) { return (int64_t)ntiles * kTcStride + 4 * 32; }
+constexpr int kItemSegs = 8;   // k_bin appends work items to 8 segments (workgroup b to segment b % 8)
+// counts, then the control block: head, fix_count, done, the 8 segments' item counts
+inline int64_t tc_words(int ntiles) { return (int64_t)ntiles * kTcStride + (3 + kItemSegs) * 32; }
 
 // The per-scene moment tables hold D = n S_bb - S_b^2 (int32) where the
 // scorer stages them in LDS (V <= 48: k_score_tab's tile rows; V > 64:
 // k_score_mma_v) and w = 1/sqrt(D) (binary64) for 48 < V <= 64.
-inline bool moments_dtab(int V) { return V <= 48 || V > 64; }
+// k_score_tab stages the tile's table rows in LDS up to this V (its VP; A/B
+// switch, 0 = never): measured slower at dinoRing (one buffer set per
+// workgroup: 121 vs 110 us; one workgroup per CU with two sets: 135 us)
+#ifndef MVS_TAB_LT_VIEWS
+#define MVS_TAB_LT_VIEWS 0
+#endif
+inline bool moments_dtab(int V) { return V <= MVS_TAB_LT_VIEWS || V > 64; }
 
 struct TiledArgs {
     int ntx, nty, ntiles;
@@ -95,7 +104,8 @@ struct TiledArgs {
     int2* sorted;
     int4* fix_list;
     int32_t* fix_count;
-    int32_t* n_items;
+    int32_t* n_items;          // kItemSegs counters, 32 ints apart: items in each segment
+    int item_seg;              // capacity of a segment (items of segment x at x * item_seg)
     int32_t* done;
     // view groups of 64 (V > 64: k_score_mma_v scores each work item against
     // every group in turn); groups = 1 otherwise

@@ -359,7 +359,8 @@ DEV int items_opened(const TiledArgs& t, int base, int c) {
 // global-histogram path of very large images)
 DEV void open_items(const TiledArgs& t, int tile, int base, int c) {
     for (int j = (base + t.chunk - 1) / t.chunk; j * t.chunk < base + c && j * t.chunk < t.cap; ++j)
-        t.items[atomicAdd(t.n_items, 1)] = make_int4(tile, j, 0, 0);
+        t.items[(blockIdx.x % kItemSegs) * t.item_seg + atomicAdd(&t.n_items[32 * (blockIdx.x % kItemSegs)], 1)] =
+            make_int4(tile, j, 0, 0);
 }
 
 template <bool LDSHIST>
@@ -457,7 +458,9 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         if (threadIdx.x == 0) {
             int run = 0;
             for (int w = 0; w < kBinBlock / 64; ++w) { const int c = s_open[w]; s_open[w] = run; run += c; }
-            s_open[kBinBlock / 64] = run ? atomicAdd(t.n_items, run) : 0;
+            // this workgroup's segment: 1/8 of the grid's atomics on each counter
+            s_open[kBinBlock / 64] = (blockIdx.x % kItemSegs) * t.item_seg +
+                                     (run ? atomicAdd(&t.n_items[32 * (blockIdx.x % kItemSegs)], run) : 0);
         }
         __syncthreads();
         int slot = s_open[kBinBlock / 64] + s_open[threadIdx.x >> 6] + incl - nopen;
@@ -653,7 +656,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
-    const int n_units = *t.n_items;
+    ItemMap im;
+    im.load(t);
+    const int n_units = im.total();
     int32_t* head = t.head;
 
     // The region of an item (gv rows, signed bytes) goes to LDS by LDS-DMA
@@ -715,13 +720,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
     int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
     int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
     if (cur >= n_units) return;
-    int4 dcur = item_desc(t, items, cur);
+    int4 dcur = item_desc(t, items, im, cur);
     dcur = make_int4(__builtin_amdgcn_readfirstlane(dcur.x), __builtin_amdgcn_readfirstlane(dcur.y),
                      __builtin_amdgcn_readfirstlane(dcur.z), 0);
     stage(dcur, std::integral_constant<int, 0>{});
     // item nx1's descriptor (uniform, scalar loads) and thread 0's claim of
     // the item after it
-    int4 dnx1 = nx1 < n_units ? item_desc(t, items, nx1) : make_int4(0, 0, 0, 0);
+    int4 dnx1 = nx1 < n_units ? item_desc(t, items, im, nx1) : make_int4(0, 0, 0, 0);
     int pend = 0;
     if (tid == 0) pend = atomicAdd(head, 1);
     __syncthreads();   // everyone has read s_ids before they are rewritten
@@ -896,7 +901,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
             }
             int4 dnx2 = make_int4(0, 0, 0, 0);
             if (nx2 < n_units) {
-                dnx2 = item_desc(t, items, nx2);
+                dnx2 = item_desc(t, items, im, nx2);
                 if (tid == 0) pend = atomicAdd(head, 1);
             }
     
@@ -1348,7 +1353,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     double* rsum = (double*)(smem + L.rsum);
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
-    const int n_items = *t.n_items;
+    ItemMap im;
+    im.load(t);
+    const int n_items = im.total();
     int32_t* head = t.head;
 
     // region piece k (view k / 2RPV, row, half) of view group g at a tile: its
@@ -1395,7 +1402,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     __syncthreads();
     int item = __builtin_amdgcn_readfirstlane(s_item);
     if (item >= n_items) return;
-    int4 d = item_desc(t, items, item);
+    int4 d = item_desc(t, items, im, item);
     stage_cands(d);
     stage_region(d.x, 0, std::integral_constant<int, 0>{});
     __syncthreads();
@@ -1588,7 +1595,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 }
                 lds_barrier();
                 next = __builtin_amdgcn_readfirstlane(s_item);
-                if (next < n_items) dn = item_desc(t, items, next);
+                if (next < n_items) dn = item_desc(t, items, im, next);
             }
             STAMP(t1);
             prefetch();
@@ -1821,7 +1828,7 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
     __syncthreads();
     if (threadIdx.x == 0 && atomicAdd(t.done, 1) == active - 1) {
         *t.fix_count = 0;
-        *t.n_items = 0;
+        for (int x = 0; x < kItemSegs; ++x) t.n_items[32 * x] = 0;
         *t.head = 0;
         *t.done = 0;
     }
@@ -2041,6 +2048,7 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 constexpr int kAccThreads = 256, kAccPer = 8, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
 constexpr int kAccE = kAccPer * kAccWaves;          // (j, wave) counts of a chunk
 constexpr int kAccEpl = (kAccE + 63) / 64;          // of them per lane of wave 0's scan
+constexpr int kAccLB = 8;                            // status words per lane of the look-back window
 static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the status words by MVS_ACC_CHUNK");
 static_assert(kAccE <= 128, "wave 0 scans at most two (j, wave) counts per lane");
 
@@ -2145,7 +2153,9 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 ex += x[q];
             }
             const uint64_t T = (uint32_t)__shfl(incl, 63, 64);   // this chunk's accepted
-            // publish, then look back over the 64 chunks before b at a time
+            // publish, then look back over the kAccLB x 64 chunks before b at
+            // a time (a 2^20 slice's 512 chunks in one window: one round of
+            // status loads once the predecessors have published)
             if (lane == 0)
                 __hip_atomic_store(&status[b], E | ((b == 0 ? 2ull : 1ull) << 32) | T, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -2153,27 +2163,40 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             int64_t top = b - 1;          // the window's highest chunk
             uint32_t spins = 0;
             bool slow = debug < 0 && b == -debug;
+            constexpr int WIN = 64 * kAccLB;
             while (top >= 0 && !slow) {
-                const int64_t k = top - lane;
-                uint64_t v = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                    : (E | (2ull << 32));
-                const bool pub = (v & ~((1ull << 34) - 1)) == E;
-                const uint32_t flag = pub ? (uint32_t)(v >> 32) & 3u : 0u;
+                // lane l, word j: chunk top - (64 j + l), at distance 64 j + l
+                uint64_t v[kAccLB];
+#pragma unroll
+                for (int j = 0; j < kAccLB; ++j) {
+                    const int64_t k = top - lane - 64 * j;
+                    v[j] = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : (E | (2ull << 32));
+                }
                 // the nearest inclusive word, and whether every chunk up to it has published
-                const uint64_t incl_m = __ballot(flag == 2), unpub = __ballot(!pub);
-                const int first_incl = incl_m ? __builtin_ctzll(incl_m) : 64;
-                const int first_unpub = unpub ? __builtin_ctzll(unpub) : 64;
-                if (first_unpub < first_incl && first_unpub < 64) {
+                int d_incl = WIN, d_unpub = WIN;
+#pragma unroll
+                for (int j = 0; j < kAccLB; ++j) {
+                    const bool pub = (v[j] & ~((1ull << 34) - 1)) == E;
+                    const uint32_t flag = pub ? (uint32_t)(v[j] >> 32) & 3u : 0u;
+                    const uint64_t im = __ballot(flag == 2), um = __ballot(!pub);
+                    if (d_incl == WIN && im) d_incl = 64 * j + __builtin_ctzll(im);
+                    if (d_unpub == WIN && um) d_unpub = 64 * j + __builtin_ctzll(um);
+                }
+                if (d_unpub < d_incl) {
                     if (++spins > spin_limit) slow = true;
                     continue;                   // a chunk in the window has not published yet
                 }
-                // lanes 0..min(first_incl, 63) hold published words to sum
-                uint64_t val = (lane <= first_incl && k >= 0) ? (v & 0xffffffffull) : 0ull;
+                // the published words at distances 0..d_incl
+                uint64_t val = 0;
+#pragma unroll
+                for (int j = 0; j < kAccLB; ++j)
+                    if (64 * j + lane <= d_incl && top - lane - 64 * j >= 0) val += v[j] & 0xffffffffull;
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
                 excl += val;
-                if (first_incl < 64) break;     // reached an inclusive prefix
-                top -= 64;
+                if (d_incl < WIN) break;        // reached an inclusive prefix
+                top -= WIN;
             }
             if (lane == 0) {
                 if (!slow) {

@@ -111,8 +111,30 @@ DEV void static_for(F&& f) {
 // Work item v of the tiled scorers: (tile, first bucket entry, candidates)
 // from the (tile, chunk j) that k_bin opened and the tile's final count
 // (uniform: scalar loads)
-DEV int4 item_desc(const TiledArgs& t, const int4* __restrict__ items, int v) {
-    const int4 it = items[v];
+// The work items k_bin appended to kItemSegs segments (one n_items atomic per
+// workgroup and segment, not one chain over the whole grid), as one list:
+// item v of the list is entry v - pre[x] of segment x, pre[x] <= v < pre[x+1]
+struct ItemMap {
+    int pre[kItemSegs + 1];
+    int seg;
+    DEV void load(const TiledArgs& t) {
+        pre[0] = 0;
+#pragma unroll
+        for (int x = 0; x < kItemSegs; ++x) pre[x + 1] = pre[x] + t.n_items[32 * x];
+        seg = t.item_seg;
+    }
+    DEV int total() const { return pre[kItemSegs]; }
+    DEV int slot(int v) const {
+        int s = v;
+#pragma unroll
+        for (int x = 1; x < kItemSegs; ++x)
+            if (v >= pre[x]) s = x * seg + v - pre[x];
+        return s;
+    }
+};
+
+DEV int4 item_desc(const TiledArgs& t, const int4* __restrict__ items, const ItemMap& im, int v) {
+    const int4 it = items[im.slot(v)];
     const int cnt = min(t.tile_count[it.x * kTcStride], t.cap);
     return make_int4(it.x, it.x * t.cap + it.y * t.chunk, min(cnt - it.y * t.chunk, t.chunk), 0);
 }

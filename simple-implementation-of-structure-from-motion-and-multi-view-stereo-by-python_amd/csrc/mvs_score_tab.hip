@@ -156,7 +156,14 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #define TSTAMP_ADD(slot, val)
 #endif
 
-constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = 512;
+// MVS_TAB_ONE (A/B switch): one workgroup per CU with all 160 KiB of LDS (two
+// waves per SIMD, 256 VGPRs each): region, list and table rows double-buffered
+#ifndef MVS_TAB_ONE
+#define MVS_TAB_ONE 0
+#endif
+constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
+constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
+constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
 constexpr int kTabChunk = MVS_MMA_CHUNK;
 
 // a candidate's constants in a unit (per wave, 32 slots)
@@ -177,9 +184,11 @@ struct TabGeom {
     // VP views) staged in LDS next to one region and list buffer, where two
     // workgroups per CU still fit (80 KiB each): V <= 48 at every WID
     static constexpr int TS = 8 * 16 * VP * 2, TD = 8 * 16 * VP * 4;
-    static constexpr bool LT = (RB + 16) + CB + TS + TD + FIXED <= 80 * 1024 - 512;
-    // else two buffers of region and list where they fit (global table reads)
-    static constexpr bool DB = !LT && 2 * (RB + 16) + 2 * CB + FIXED <= 80 * 1024 - 512;
+    static constexpr int BUF = (RB + 16) + CB + (VP <= MVS_TAB_LT_VIEWS ? TS + TD : 0);   // one item's LDS
+    static constexpr bool LT = VP <= MVS_TAB_LT_VIEWS;
+    static_assert(BUF + FIXED <= kTabBudget, "one item's buffers fit");
+    // two buffer sets where they fit: item k+1's lands while item k is scored
+    static constexpr bool DB = 2 * BUF + FIXED <= kTabBudget;
 };
 
 // w = 1/sqrt(D): the two instructions k_moments uses for its w table (bit
@@ -191,7 +200,7 @@ DEV double w_of(int db) {
 }
 
 template <int WID, int NBLK, bool FAST>
-__global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
+__global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
                                                                const MomentsDev mt, const int4* __restrict__ items,
                                                                const int2* __restrict__ sorted) {
     using G = MmaGeom<WID>;
@@ -199,7 +208,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     constexpr int NB = G::NB, NPX = G::NPX, KS = G::KS, VS = G::VS, C0 = G::C0;
     constexpr int VP = TG::VP;
     constexpr bool DB = TG::DB, LT = TG::LT;
-    static_assert(LT == (NBLK <= 3), "the host builds D tables (moments_dtab) exactly for V <= 48");
+
     constexpr int RPV = VS / 32;                                          // region rows per view incl. the pad row
     constexpr int PF = (VP * RPV * 2 + kTabThreads - 1) / kTabThreads;    // 16-B pieces per thread
     constexpr int RB = TG::RB, CB = TG::CB;
@@ -209,9 +218,8 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB + 16], s_reg1[DB ? RB + 16 : 16];
     __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[DB ? CB : 16];
     __shared__ __attribute__((aligned(16))) TabInfo s_ti[kTabWaves * 32];
-    __shared__ __attribute__((aligned(16))) uint8_t s_tab[LT ? TG::TS + TG::TD : 16];   // LT: [S_b rows][D rows]
-    const int16_t* ls_sb = (const int16_t*)s_tab;
-    const int32_t* ls_d = (const int32_t*)(s_tab + (LT ? TG::TS : 0));
+    // LT: the tile's table rows, [S_b rows][D rows]
+    __shared__ __attribute__((aligned(16))) uint8_t s_tab0[LT ? TG::TS + TG::TD : 16], s_tab1[LT && DB ? TG::TS + TG::TD : 16];
     __shared__ int s_ids[2];
     __shared__ double s_recip[65];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -225,13 +233,16 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
-    const int n_units = *t.n_items;
+    ItemMap im;
+    im.load(t);
+    const int n_units = im.total();
     int32_t* head = t.head;
     const int16_t* __restrict__ tsb = mt.sb;
     const double* __restrict__ tw = mt.w;
 
     auto region_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_reg1 : s_reg0; };
     auto cand_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_cand1 : s_cand0; };
+    auto tab_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_tab1 : s_tab0; };
     // the item's region (gv rows) and sorted (id, pk) entries by LDS-DMA
     auto stage = [&](const int4 d, auto bufc) {
         const int ty = d.x / t.ntx, tx = d.x - ty * t.ntx;
@@ -270,7 +281,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
                         src = (const uint8_t*)(mt.d + px * VP) + 16 * c;
                     }
                     __builtin_amdgcn_global_load_lds((const void*)src,
-                                                     (void __attribute__((address_space(3)))*)(s_tab + (p * kTabThreads + wave * 64) * 16),
+                                                     (void __attribute__((address_space(3)))*)(tab_buf(bufc) + (p * kTabThreads + wave * 64) * 16),
                                                      16, 0, 0);
                 }
             }
@@ -300,7 +311,7 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
     // vector loads (a lane-dependent-looking address): their wait is the
     // in-order vmcnt at the round's end, not lgkmcnt(0) in front of every LDS
     // read of the round
-    auto item_v = [&](int v) -> int2 { return *(const int2*)(items + opaque(v)); };
+    auto item_v = [&](int v) -> int2 { return *(const int2*)(items + opaque(im.slot(v))); };
     auto count_v = [&](int tile) -> int { return t.tile_count[opaque(tile * kTcStride)]; };
     // the item pipeline: while item k is scored, item k+1's region and list
     // (DB) and its tile's count, item k+2's (tile, chunk) and thread 0's claim
@@ -330,6 +341,8 @@ __global__ __launch_bounds__(kTabThreads, 4) void k_score_tab(const SceneDev sc,
         const int nc = dcur.z;
         const uint8_t* reg = region_buf(bufc);
         int2* cand = (int2*)cand_buf(bufc);
+        const int16_t* ls_sb = (const int16_t*)tab_buf(bufc);
+        const int32_t* ls_d = (const int32_t*)(tab_buf(bufc) + (LT ? TG::TS : 0));
         const int zoff = RB;   // the zero row, relative to the region buffer
         // ---- 1. this item's region and list have landed (every wave's DMA) ----
         TSTAMP(ts0);

@@ -39,3 +39,15 @@ print(f"wid {wid}: items {items:.0f} over {(d[:, 0] > 0).sum()} workgroups; M-bl
 for k, name in [(1, "barrier wait (round start)"), (2, "sort"), (3, "units"), (5, "  K-loops"), (6, "  epilogues")]:
     print(f"  {name:28s} {d[:, k].sum() / waves:9.0f} cycles per (item, wave)")
 print(f"  per M-block: K-loop {d[:, 5].sum() / d[:, 4].sum():.0f}, epilogue {d[:, 6].sum() / d[:, 4].sum():.0f} cycles")
+# k_bin's phases (rows 2048+ of the mvs_kernels stamps)
+lib.mvs_read_stamps.argtypes = [ctypes.c_void_p]
+kbuf = np.zeros(4096 * 16, np.uint64)
+lib.mvs_read_stamps(kbuf.ctypes.data)
+k0 = kbuf.copy()
+ctx.score(c, ref, 0.7, wid)
+lib.mvs_read_stamps(kbuf.ctypes.data)
+kb = (kbuf - k0).reshape(4096, 16)[2048:].astype(np.float64)
+kact = kb[:, 0] > 0
+if kact.any():
+    print(f"  k_bin: {kact.sum()} workgroups; per workgroup: loads + projection + LDS ranks {kb[kact, 1].mean():.0f}, "
+          f"global tile bases + items {kb[kact, 2].mean():.0f}, bucket writes {kb[kact, 3].mean():.0f} cycles")
