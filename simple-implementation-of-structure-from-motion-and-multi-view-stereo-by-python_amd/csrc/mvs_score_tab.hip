@@ -145,7 +145,8 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
 #ifdef MVS_STAMPS
 // diagnostic build only: per-workgroup cycle sums (lane 0 of every wave adds
 // its own): slot 0 rounds (wave 0), 1 barrier wait at the round's start, 2
-// the wave's sort, 3 its units, 4 its M-blocks, 5 K-loops, 6 epilogues;
+// the wave's sort (from the barrier: incl. 7), 3 its units, 4 its M-blocks,
+// 5 K-loops, 6 epilogues, 7 the next item's LDS-DMA issue and loads;
 // read by mvs_read_stamps_tab
 __device__ unsigned long long g_stamps_tab[1024 * 16];
 #define TSTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
@@ -286,15 +287,17 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 }
             }
         }
+        // the list in 16-B pieces (two entries; bucket starts are 512-B
+        // aligned and d.w even): one DMA instruction per wave for a chunk
         uint8_t* cbase = cand_buf(bufc);
-        const int32_t* csrc = (const int32_t*)(sorted + d.y);
+        const uint8_t* csrc = (const uint8_t*)(sorted + d.y);
 #pragma unroll
-        for (int p = 0; p < 2 * kTabChunk / kTabThreads; ++p) {
+        for (int p = 0; p < (kTabChunk / 2 + kTabThreads - 1) / kTabThreads; ++p) {
             const int k = tid + p * kTabThreads;
-            if (k < 2 * d.w)
-                __builtin_amdgcn_global_load_lds((const void*)(csrc + k),
-                                                 (void __attribute__((address_space(3)))*)(cbase + (p * kTabThreads + wave * 64) * 4),
-                                                 4, 0, 0);
+            if (k < d.w / 2)
+                __builtin_amdgcn_global_load_lds((const void*)(csrc + 16 * k),
+                                                 (void __attribute__((address_space(3)))*)(cbase + (p * kTabThreads + wave * 64) * 16),
+                                                 16, 0, 0);
         }
     };
 
@@ -363,6 +366,8 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         const int2 it2 = item_v(min(nx2, n_units - 1));
         const int c1 = count_v(it1.x);
         if (nx2 < n_units && tid == 0) pend = claim();
+        TSTAMP(ts1b);
+        TSTAMP_ADD(7, ts1b - ts1);
         const int ty = dcur.x / t.ntx, tx = dcur.x - ty * t.ntx;
         const int tix0 = ((ty * MVS_TILE_H) * sc.W + tx * MVS_TILE_W) * VP;   // table element of the tile origin
         // ---- 2. this wave's M-blocks, sorted by row pair inside the wave ----

@@ -283,13 +283,22 @@ def _smooth_ring(pkg, V, H=96, W=128):
     return rgb, K, R, t
 
 
+@pytest.mark.parametrize("mode", ["", "tab"])
 @pytest.mark.parametrize("V,wid", [(68, 5), (100, 3), (256, 3), (100, 1), (132, 2), (200, 4)])
-def test_view_groups_wid_and_partial_group(pkg, orc, V, wid):
-    """The view-group path of k_score_mma (V > 64) with a 4-view last group
-    (V = 68), every window size."""
+def test_view_groups_wid_and_partial_group(pkg, orc, V, wid, mode):
+    """The view-group path k_score_mma_v (V > 64) with a 4-view last group
+    (V = 68), every window size; in-kernel moments (default) and the D tables
+    (MVS_SCORE_KERNEL=tab)."""
+    import os
     H, W = 96, 128
     rgb, K, R, t = _smooth_ring(pkg, V, H, W)
-    with pkg.MvsContext(rgb, K, R, t) as cx:
+    if mode:
+        os.environ["MVS_SCORE_KERNEL"] = mode
+    try:
+        cx = pkg.MvsContext(rgb, K, R, t)
+    finally:
+        os.environ.pop("MVS_SCORE_KERNEL", None)
+    with cx:
         sc = orc.Scene(rgb, K, R, t)
         c, ref = pkg.synthetic.candidates(3000, K, R, t, W=W, H=H, seed=2)
         for thr in (0.2, 0.6):

@@ -36,7 +36,8 @@ d = (buf - before).reshape(1024, 16)[:512].astype(np.float64)
 items = d[:, 0].sum()
 waves = items * 8
 print(f"wid {wid}: items {items:.0f} over {(d[:, 0] > 0).sum()} workgroups; M-blocks {d[:, 4].sum():.0f}")
-for k, name in [(1, "barrier wait (round start)"), (2, "sort"), (3, "units"), (5, "  K-loops"), (6, "  epilogues")]:
+for k, name in [(1, "barrier wait (round start)"), (2, "DMA issue + sort"), (7, "  DMA issue + loads"), (3, "units"),
+                (5, "  K-loops"), (6, "  epilogues")]:
     print(f"  {name:28s} {d[:, k].sum() / waves:9.0f} cycles per (item, wave)")
 print(f"  per M-block: K-loop {d[:, 5].sum() / d[:, 4].sum():.0f}, epilogue {d[:, 6].sum() / d[:, 4].sum():.0f} cycles")
 # k_bin's phases (rows 2048+ of the mvs_kernels stamps)
