@@ -440,7 +440,7 @@ def main():
             del os.environ["MVS_SCORER_WGS"]
         ov["scorer_448_workgroups"] = {k: v for k, v in overlap_proxy(
             ctx2, sw, V, vlb, accepted, stream, a.thr, a.wid, max(a.steps // 2, 10)).items()
-            if k.endswith("_us")}
+            if "_us" in k}
         ctx2.close()
         out["exchange"]["overlap_proxy"] = ov
 
