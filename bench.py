@@ -18,7 +18,7 @@ Beside the headline (rank 0 at N = 1 only, so that the driver's N > 1 runs
 stay short):
   roofline     the binding roof of the dominant kernel (k_score_mma) from the
                live kernel time and the per-launch counters of the committed
-               rocprofv3 PMC profile (profiles/r03/pmc.json): HBM bytes,
+               rocprofv3 PMC profile (profiles/r04/pmc.json): HBM bytes,
                VALU-busy cycles, MFMA i8 operations; frac <= 1 each
   cold_sweep   scene setup from the resident images (k_build_scene) + the sweep
   secondary    wid 3 (BASELINE config 2's 7x7 window)
