@@ -320,11 +320,10 @@ struct mvs_ctx {
     DevBuf<int32_t> f_rows, f_pts, f_mom, f_best;
     int kernel_mode = 0;   // 0 auto, 1 direct, 2 tiled (env MVS_SCORE_KERNEL)
     // the tiled scorer's window moments: per wid, built on first use
-    // (k_moments), rebuilt with the scene; tab_mode 0 = tables when V <= 64
-    // and they fit, 1 = never (the in-kernel moments of k_score_mma; env
-    // MVS_SCORE_KERNEL=mma), 2 = also for V > 64 (k_score_mma_v<TAB>; env
-    // MVS_SCORE_KERNEL=tab: at ring256 its D-table gathers measured 1.86 ms
-    // per 2^20 against 1.70 ms for the in-kernel Q table, so not the default)
+    // (k_moments), rebuilt with the scene; tab_mode 0 = tables when they fit
+    // (ring256 with tile-order items: 1.52 ms per 2^20 against 1.67-1.69 ms
+    // for the in-kernel Q table), 1 = never (in-kernel moments; env
+    // MVS_SCORE_KERNEL=mma), 2 = tables (env MVS_SCORE_KERNEL=tab)
     int tab_mode = 0;
     int scorer_wgs = 0;   // env MVS_SCORER_WGS: k_score_tab's grid (0 = every CU, twice)
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
@@ -347,7 +346,7 @@ struct mvs_ctx {
     // past the end: k_score_tab stages a tile's rows whole (16 pixels x VP),
     // also where the last tile column runs past W
     bool ensure_moments(int wid, hipStream_t s) {
-        if (tab_mode == 1 || (tab_mode == 0 && V > MVS_GROUP_VIEWS)) return false;
+        if (tab_mode == 1) return false;
         const int64_t elems = ((int64_t)H * W + 16) * moments_vp();
         if (elems >= ((int64_t)1 << 31)) return false;
         if (!mom_ok[wid]) {

@@ -346,21 +346,43 @@ __device__ unsigned long long g_stamps[4096 * 16];
 constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
 constexpr int kMmaGrid = 256;         // the scorers' workgroups: one per CU; the queue balances
 
-// the number of work items ranks [base, base + c) of a tile open: chunk j
-// (bucket entries [j chunk, (j+1) chunk), below cap) opens with rank j chunk
-DEV int items_opened(const TiledArgs& t, int base, int c) {
-    if (c <= 0) return 0;
-    const int lo = (base + t.chunk - 1) / t.chunk;
-    const int hi = (min(base + c, t.cap) + t.chunk - 1) / t.chunk;
-    return max(hi - lo, 0);
-}
-
-// items opened by ranks [base, base + c) of a tile (one atomic each: the
-// global-histogram path of very large images)
-DEV void open_items(const TiledArgs& t, int tile, int base, int c) {
-    for (int j = (base + t.chunk - 1) / t.chunk; j * t.chunk < base + c && j * t.chunk < t.cap; ++j)
-        t.items[(blockIdx.x % kItemSegs) * t.item_seg + atomicAdd(&t.n_items[32 * (blockIdx.x % kItemSegs)], 1)] =
-            make_int4(tile, j, 0, 0);
+// The work items in tile order: one workgroup reads every tile's count, scans
+// the tiles' chunk counts (chunk j of a tile: bucket entries [j chunk,
+// (j+1) chunk) below min(count, cap)) and writes (tile, j) for each chunk into
+// segment 0 (the other segments' counts to 0).  Measured against items in the
+// order k_bin's workgroups opened them (same box): k_score_mma_v at ring256
+// 1.67-1.72 vs 1.86-1.87 ms per 2^20, k_score_tab at dinoRing 105.5-107.2 vs
+// 111.1-111.6 us (profiles/r04/r4r_*, r4s_*).
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_item_scan(const TiledArgs t) {
+    __shared__ int s_w[kScanThreads / 64 + 1];
+    const int per = (t.ntiles + kScanThreads - 1) / kScanThreads;   // tiles per thread, contiguous
+    const int t0 = min((int)threadIdx.x * per, t.ntiles), t1 = min(t0 + per, t.ntiles);
+    int mine = 0;
+    for (int k = t0; k < t1; ++k) {
+        const int c = min(t.tile_count[k * kTcStride], t.cap);
+        mine += (c + t.chunk - 1) / t.chunk;
+    }
+    int incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d, 64);
+        if ((threadIdx.x & 63) >= d) incl += o;
+    }
+    if ((threadIdx.x & 63) == 63) s_w[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) { const int c = s_w[w]; s_w[w] = run; run += c; }
+        s_w[kScanThreads / 64] = run;
+    }
+    __syncthreads();
+    int slot = s_w[threadIdx.x >> 6] + incl - mine;
+    for (int k = t0; k < t1; ++k) {
+        const int c = min(t.tile_count[k * kTcStride], t.cap);
+        for (int j = 0; j * t.chunk < c; ++j) t.items[slot++] = make_int4(k, j, 0, 0);
+    }
+    if (threadIdx.x < kItemSegs) t.n_items[32 * threadIdx.x] = threadIdx.x == 0 ? s_w[kScanThreads / 64] : 0;
 }
 
 template <bool LDSHIST>
@@ -371,7 +393,6 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     // candidate reads its reference camera's 16 values there instead of by
     // per-lane global loads
     __shared__ double s_cam[MVS_MAX_VIEWS][16];
-    __shared__ int s_open[kBinBlock / 64 + 1];
     const int words = (sc.V + 63) >> 6;
     for (int k = threadIdx.x; k < sc.V * 16; k += blockDim.x) {
         const int v = k >> 4, f = k & 15;
@@ -423,7 +444,6 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             lr[k] = atomicAdd(&hist[tile], 1);
         } else {
             lr[k] = atomicAdd(&t.tile_count[tile * kTcStride], 1);
-            open_items(t, tile, lr[k], 1);
         }
     }
     STAMP(t1);
@@ -438,41 +458,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             const int c = b < t.ntiles ? hist[b] : 0;
             bs[j] = c ? atomicAdd(&t.tile_count[b * kTcStride], c) : 0;
         }
-        // the work items this workgroup opens (chunk starts j chunk inside a
-        // returned rank range), appended with ONE n_items atomic per
-        // workgroup: slot = its base + the thread's exclusive prefix
-        int nopen = 0;
 #pragma unroll
         for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
             const int b = threadIdx.x + j * kBinBlock;
-            if (b < t.ntiles) nopen += items_opened(t, bs[j], hist[b]);
-        }
-        int incl = nopen;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int o = __shfl_up(incl, d, 64);
-            if ((threadIdx.x & 63) >= d) incl += o;
-        }
-        if ((threadIdx.x & 63) == 63) s_open[threadIdx.x >> 6] = incl;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int run = 0;
-            for (int w = 0; w < kBinBlock / 64; ++w) { const int c = s_open[w]; s_open[w] = run; run += c; }
-            // this workgroup's segment: 1/8 of the grid's atomics on each counter
-            s_open[kBinBlock / 64] = (blockIdx.x % kItemSegs) * t.item_seg +
-                                     (run ? atomicAdd(&t.n_items[32 * (blockIdx.x % kItemSegs)], run) : 0);
-        }
-        __syncthreads();
-        int slot = s_open[kBinBlock / 64] + s_open[threadIdx.x >> 6] + incl - nopen;
-#pragma unroll
-        for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
-            const int b = threadIdx.x + j * kBinBlock;
-            if (b < t.ntiles) {
-                const int c = hist[b];
-                for (int q = (bs[j] + t.chunk - 1) / t.chunk; c && q * t.chunk < bs[j] + c && q * t.chunk < t.cap; ++q)
-                    t.items[slot++] = make_int4(b, q, 0, 0);
-                hist[b] = bs[j];
-            }
+            if (b < t.ntiles) hist[b] = bs[j];
         }
         __syncthreads();
     }
@@ -2049,6 +2038,11 @@ constexpr int kAccThreads = 256, kAccPer = 8, kAccChunk = kAccThreads * kAccPer,
 constexpr int kAccE = kAccPer * kAccWaves;          // (j, wave) counts of a chunk
 constexpr int kAccEpl = (kAccE + 63) / 64;          // of them per lane of wave 0's scan
 constexpr int kAccLB = 8;                            // status words per lane of the look-back window
+// 16-B accesses at 8-B alignment (global_load/store_dwordx4 allow it)
+typedef double acc_d2v __attribute__((ext_vector_type(2)));
+typedef acc_d2v acc_d2 __attribute__((aligned(8)));
+typedef long long acc_l2v __attribute__((ext_vector_type(2)));
+typedef acc_l2v acc_l2 __attribute__((aligned(8)));
 static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the status words by MVS_ACC_CHUNK");
 static_assert(kAccE <= 128, "wave 0 scans at most two (j, wave) counts per lane");
 
@@ -2122,8 +2116,10 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             m[j] = __ballot(acc);
             px[j] = py[j] = pz[j] = 0.0;
             if (cpt && acc) {
-                px[j] = cpt[3 * i];
-                py[j] = cpt[3 * i + 1];
+                // x, y as one 16-B load (8-B aligned), z beside it
+                const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
+                px[j] = xy.x;
+                py[j] = xy.y;
                 pz[j] = cpt[3 * i + 2];
             }
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
@@ -2250,7 +2246,13 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
                                     __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
-                if (pos < cap) {
+                if (pos < cap && words == 1 && cpt) {
+                    // the 40-B row as 16 + 16 + 8 B (8-B aligned stores)
+                    int64_t* o = out + (1 + pos) * width;
+                    *(acc_l2*)o = acc_l2{offset + i, (int64_t)w0[j]};
+                    *(acc_l2*)(o + 2) = acc_l2{__double_as_longlong(px[j]), __double_as_longlong(py[j])};
+                    o[4] = __double_as_longlong(pz[j]);
+                } else if (pos < cap) {
                     int64_t* o = out + (1 + pos) * width;
                     o[0] = offset + i;
                     o[1] = (int64_t)w0[j];
@@ -2460,6 +2462,9 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         hipLaunchKernelGGL(k_bin<true>, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
     else
         hipLaunchKernelGGL(k_bin<false>, dim3(nbin), dim3(kBinBlock), 0, s, *sc, *a, *t, WID);
+    // the work items in tile order (the scorers' workgroups in flight then
+    // share image rows -- and at V > 64 table rows -- in L2)
+    hipLaunchKernelGGL(k_item_scan, dim3(1), dim3(kScanThreads), 0, s, *t);
     int rc = 0;
     {
         TimedLaunch tl(s, ev0, ev1);
