@@ -162,6 +162,9 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_ONE
 #define MVS_TAB_ONE 0
 #endif
+#ifndef MVS_TAB_PIXSORT
+#define MVS_TAB_PIXSORT 0   // A/B switch: sort a wave's candidates by pixel, not by row pair
+#endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
@@ -375,23 +378,37 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         const int b0 = (nblk * wave) >> 3, b1 = (nblk * (wave + 1)) >> 3;
         {
             const int base = 16 * b0, cnt = min(16 * b1, nc) - base;   // <= 128
-            int2 c0 = make_int2(0, 0), c1 = make_int2(0, 0);
-            int bin0 = 4, bin1 = 4;
-            if (lane < cnt) { c0 = cand[base + lane]; bin0 = (c0.y >> 5) & 3; }
-            if (lane + 64 < cnt) { c1 = cand[base + 64 + lane]; bin1 = (c1.y >> 5) & 3; }
-            int r0 = 0, r1 = 0, run = 0;
-            static_for<4>([&](auto Yc) {
-                constexpr int y = Yc;
-                const uint64_t m0 = __ballot(bin0 == y), m1 = __ballot(bin1 == y);
-                const int p0 = __popcll(m0);
-                if (bin0 == y) r0 = run + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
-                if (bin1 == y) r1 = run + p0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-                run += p0 + __popcll(m1);
-            });
-            if (lane < cnt) cand[base + r0] = c0;
-            if (lane + 64 < cnt) cand[base + r1] = c1;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            // one stable counting pass by the digit (pk >> SH) & (NBINS - 1)
+            // (ballots + mbcnt, in the wave's own part of the list)
+            auto pass = [&](auto shc, auto nbc) {
+                constexpr int SH = decltype(shc)::value, NBINS = decltype(nbc)::value;
+                int2 c0 = make_int2(0, 0), c1 = make_int2(0, 0);
+                int bin0 = NBINS, bin1 = NBINS;
+                if (lane < cnt) { c0 = cand[base + lane]; bin0 = (c0.y >> SH) & (NBINS - 1); }
+                if (lane + 64 < cnt) { c1 = cand[base + 64 + lane]; bin1 = (c1.y >> SH) & (NBINS - 1); }
+                int r0 = 0, r1 = 0, run = 0;
+                static_for<NBINS>([&](auto Yc) {
+                    constexpr int y = Yc;
+                    const uint64_t m0 = __ballot(bin0 == y), m1 = __ballot(bin1 == y);
+                    const int p0 = __popcll(m0);
+                    if (bin0 == y) r0 = run + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+                    if (bin1 == y) r1 = run + p0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+                    run += p0 + __popcll(m1);
+                });
+                if (lane < cnt) cand[base + r0] = c0;
+                if (lane + 64 < cnt) cand[base + r1] = c1;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            };
+#if MVS_TAB_PIXSORT
+            // by pixel (column, then row: LSD), which keeps the row-pair order
+            // the K-loop spans need and puts a pixel's candidates next to each
+            // other, so their table gathers share lines
+            pass(std::integral_constant<int, 0>{}, std::integral_constant<int, 16>{});
+            pass(std::integral_constant<int, 4>{}, std::integral_constant<int, 8>{});
+#else
+            pass(std::integral_constant<int, 5>{}, std::integral_constant<int, 4>{});   // row pair
+#endif
         }
         TSTAMP(ts2);
         // ---- 3. + 4. units of two M-blocks (32 consecutive sorted candidates) ----
