@@ -69,8 +69,8 @@ struct ScoreArgs {
 //   rank r of tile k at k*cap + r), pk = (x - x0) | (y - y0) << 4 | R << 7
 //   (pixel inside the tile); a candidate of rank >= cap overflows to fix_list
 //   items = (tile, chunk j, 0, 0): bucket entries [j chunk, (j+1) chunk) of
-//   the tile, appended by k_bin in the order the chunks were opened, to
-//   segment b % kItemSegs of the opening workgroup b (ItemMap: one list)
+//   the tile, written in tile order by k_item_scan into segment 0 of
+//   kItemSegs (ItemMap presents the segments as one list)
 //   fix_list[n], fix_count: {id, tile, pk, 0} of the candidates k_score_fix
 //   scores by the direct path -- bucket overflow (k_bin) and candidates with
 //   a view decision inside the guard band (the tiled scorers, numpy-order

@@ -307,11 +307,10 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
 // window and ranks the candidate inside its tile -- through an LDS histogram
 // per block (one global atomic per non-empty (block, tile) pair) when the tile
 // counters fit in LDS, else through one global atomic per candidate -- and
-// writes it into the tile's bucket.  The work items need no scan: a tile's
-// chunk j (candidates [j chunk, (j+1) chunk) of its bucket) is opened by the
-// one workgroup whose returned range of ranks covers rank j chunk, which
-// appends (tile, j) to the item list; the scorers read the tile's final count
-// when they take the item (item_desc).
+// writes it into the tile's bucket.  k_item_scan then writes the work items
+// (tile, chunk j: candidates [j chunk, (j+1) chunk) of its bucket) in tile
+// order; the scorers read the tile's final count when they take the item
+// (item_desc).
 // ---------------------------------------------------------------------------
 #ifndef MVS_BIN_PER
 #define MVS_BIN_PER 4   // candidates per k_bin thread (A/B switch)
@@ -321,7 +320,7 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
 // (slot 0 items, 1 staging + barrier, 2 moments, 3 candidates, 4 wave 0's own
 // candidate time, 5 wave 0's M-blocks), read by mvs_read_stamps; k_bin's
 // workgroups use rows 2048 + (slot 0 workgroups, 1 projection + LDS ranks,
-// 2 global tile bases and opened items, 3 bucket writes)
+// 2 global tile bases, 3 bucket writes)
 __device__ unsigned long long g_stamps[4096 * 16];
 #define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, val) \
@@ -1237,7 +1236,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
 // next item's candidate list and, behind group 0's phase 2, an item's
 // reference rows.  Every LDS-DMA target is a static LDS array of its own, so
 // that the compiler sees no aliasing with the tables phases 2-4 read and
-// write.  Work items come in the order k_bin opened them (about tile order): the workgroups in flight
+// write.  Work items come in tile order (k_item_scan): the workgroups in flight
 // share image rows, so TLB and L2 reach over 256 views of a large image.
 // ---------------------------------------------------------------------------
 constexpr int kVTab = 68;   // Q-table row pitch (int32): the per-column writes are conflict free

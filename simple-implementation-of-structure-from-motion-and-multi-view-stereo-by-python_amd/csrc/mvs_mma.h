@@ -109,9 +109,10 @@ DEV void static_for(F&& f) {
 }
 
 // Work item v of the tiled scorers: (tile, first bucket entry, candidates)
-// from the (tile, chunk j) that k_bin opened and the tile's final count
+// from the item list's (tile, chunk j) and the tile's final count
 // (uniform: scalar loads)
-// The work items k_bin appended to kItemSegs segments (one n_items atomic per
+// The work items in kItemSegs segments (k_item_scan fills segment 0; the
+// layout also takes per-workgroup appends, one n_items atomic per
 // workgroup and segment, not one chain over the whole grid), as one list:
 // item v of the list is entry v - pre[x] of segment x, pre[x] <= v < pre[x+1]
 struct ItemMap {
