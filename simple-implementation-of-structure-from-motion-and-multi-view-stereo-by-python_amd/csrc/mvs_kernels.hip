@@ -2028,7 +2028,7 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // Chunks of kAccPer x kAccThreads = 2,048 candidates, thread t of a chunk
 // holding candidates chunk + t + kAccThreads j (j < kAccPer): the reads stay
 // coalesced, a 2^20 slice has 512 chunks (two workgroups on every CU), and
-// the look-back walks at most a few 64-chunk windows.  Each candidate's first
+// the look-back reads 512-chunk windows (one window for such a slice).  Each candidate's first
 // mask word is loaded with its count (records: the count IS its popcount), the
 // accepted candidates' points as soon as the counts are in; they stay in
 // flight across the chunk's scan and look-back (LDS-only barriers), so that
