@@ -34,7 +34,11 @@ stay short):
                at fixture generation (tests/golden/reference_timing.json)
 
 python bench.py [--gpus N --steps K --warmup W --n CANDS --wid 5]
-N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+N > 1: either under a launcher (python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N ..., which must start exactly N ranks), or `python bench.py
+--gpus N` alone: the process then starts the N ranks itself as children of a
+torch.distributed.run subprocess (before touching the GPU), relays rank 0's JSON
+line and exits with the children's status.
 """
 import argparse
 import hashlib
@@ -254,6 +258,39 @@ def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups
             "proxy_alone_us": e0.elapsed_time(e1) / 10 * 1e3, "received_bytes": recv, "workgroups": workgroups}
 
 
+def launch_ranks(nranks):
+    """`bench.py --gpus N` (N > 1) without a launcher: start the N ranks as
+    children (python -m torch.distributed.run, one process per GPU, rendezvous
+    on 127.0.0.1), forward their output, print rank 0's JSON line as this
+    process's only stdout line, and return the exit status (non-zero when any
+    rank failed or no line came).  Runs before anything initialises the GPU:
+    this process never touches it."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MVS_BENCH_LAUNCHED="1")
+    line = None
+    with subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env) as p:
+        for ln in p.stdout:
+            if ln.startswith("{") and '"metric"' in ln:
+                line = ln.strip()
+            else:
+                sys.stderr.write(ln)
+                sys.stderr.flush()
+        rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    if rc == 0 and line is None:
+        print(f"bench.py: the {nranks} ranks exited without a result line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -279,13 +316,24 @@ def main():
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
                     help="headline scene (ring256: config 4 as the headline, for profiling)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # no launcher: this process starts the ranks and never touches the GPU
+        sys.exit(launch_ranks(a.gpus))
 
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)")
+    ndev = torch.cuda.device_count()
+    if world > 1 and a.backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, {ndev} visible "
+                         "(--backend gloo rehearses several ranks on one GPU)")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -293,6 +341,15 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit(f"bench.py: process group of {dist.get_world_size()} ranks, --gpus {a.gpus}")
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": local,
+          "pci_bus_id": getattr(props, "pci_bus_id", None), "name": props.name}
+    ranks_info = [me]
+    if world > 1:
+        ranks_info = [None] * world
+        dist.all_gather_object(ranks_info, me)
     pkg = importlib.import_module(PKG_NAME)
     par = importlib.import_module(PKG_NAME + ".parallel")
     syn = pkg.synthetic
@@ -342,9 +399,10 @@ def main():
             score(cx, sw, wid, a.thr, stream)
             if evs is not None:
                 evs[1].record(stream)
-            if exchange and world > 1:
-                # pack (device, no host sync) + all-gather on the exchange's own
-                # stream, overlapping the next sweep (parallel.PointsExchange)
+            if exchange and "exch" in sw:
+                # pack (device, no host sync) + at N > 1 the all-gather on the
+                # exchange's own stream, overlapping the next sweep
+                # (parallel.PointsExchange); at N = 1 the pack alone
                 sw["exch"].post(sw["off"], *pack_src(sw), vlb, stream=stream, c=sw["c"])
 
         for _ in range(warmup):
@@ -370,7 +428,7 @@ def main():
         if kl != len(timed_steps) or kt <= 0.0:
             raise RuntimeError(f"kernel timing recorded {kl} launches / {kt} ms for {len(timed_steps)} timed steps")
         pms = sum(e0.elapsed_time(e1) for e0, e1 in evs.values()) / len(evs)
-        if exchange and world > 1:
+        if exchange and "exch" in sw:
             got["n"] = int(sum(sw["exch"].accepted()))    # every rank's rows arrived, none over capacity / failed
         if world > 1:
             tt = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -393,8 +451,28 @@ def main():
     dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup)
     value = total_n * a.steps / dt
     accepted = int((host_outputs(sw)[1] >= vlb).sum())
+    acc_ranks = [accepted]
+    if world > 1:
+        acc_ranks = [None] * world
+        dist.all_gather_object(acc_ranks, accepted)
     kernel_name = ctx.timed_kernel()
     solo = rank == 0 and world == 1
+    scaling_base = None
+    if solo:
+        # the N = 1 step with the N > 1 step's device work minus the gather:
+        # score + the 40-B point pack (PointsExchange at world 1), so that a
+        # 1 -> N comparison can also be made on the same device work
+        cap1 = accepted + accepted // 16 + 256
+        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap1, dev)
+        pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup)
+        del sw["exch"]
+        if packed != accepted:
+            raise RuntimeError(f"N = 1 pack: {packed} rows != {accepted} accepted")
+        scaling_base = {"step_ms_with_pack": pdt / a.steps * 1e3, "value_with_pack": n * a.steps / pdt,
+                        "step_ms_score_only": dt / a.steps * 1e3,
+                        "note": "`value` at N = 1 is the scoring step alone (no exchange exists on one GPU); "
+                                "at N > 1 a step adds the 40-B point pack and the all-gather (overlapped "
+                                "with the next sweep). value_with_pack is the N = 1 step with the pack"}
 
     out = {
         "metric": ("candidate patches/sec NCC-scored (640×480, 48 views) at 1/2/4/8 MI355X; % HBM roofline"
@@ -416,11 +494,19 @@ def main():
         "config": {"workload": f"{'dinoRing' if a.scene == 'dino' else 'sphere ring'} {V}x{W}x{H}, "
                                f"one expansion sweep of {n} candidates per GPU, "
                                f"{2 * a.wid + 1}x{2 * a.wid + 1} NCC (wid={a.wid}) vs all views, "
-                               f"MIN_NCC {a.thr}, accepted points (index, view mask, x y z) all-gathered",
+                               f"MIN_NCC {a.thr}" +
+                               (", accepted points (index, view mask, x y z) packed and all-gathered"
+                                if world > 1 else ", one GPU (no exchange)"),
                    "global_batch": total_n, "wid": a.wid, "views": V,
                    "outputs": ("per candidate: xy + mask, count, avg arrays" if a.soa else
                                "per candidate: xy + one record [mask word, avg] (|V| = popcount)"),
-                   "parallelism": f"candidate-queue shards x{world} (RCCL all-gather of accepted points)"},
+                   "parallelism": (f"candidate-queue shards x{world} ({'RCCL' if a.backend == 'nccl' else 'gloo'} "
+                                   f"all-gather of accepted points)" if world > 1 else "single GPU")},
+        "ranks_seen": len(ranks_info),
+        "backend": (a.backend if world > 1 else None),
+        "ranks": ranks_info,
+        "accepted_per_rank": acc_ranks,
+        "scaling_baseline": scaling_base,
         "kernel": kernel_name,
         "kernel_timing": f"HIP events around the scorer on every {TIME_EVERY}th timed step",
         "score_call_ms": pms,

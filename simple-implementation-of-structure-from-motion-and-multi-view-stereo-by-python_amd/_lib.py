@@ -332,8 +332,15 @@ class MvsContext:
         stream-ordered, no host sync.  count None: mask is score_device_rec's
         records and |V| their popcount."""
         n = int(count.numel()) if count is not None else int(mask.shape[0])
-        if count is None and (mask.dtype.itemsize != 8 or mask.shape[1] != self.words + 1):
-            raise RuntimeError("pack_accepted: records must be int64 (n, words + 1)")
+        # the kernel indexes rows at a fixed pitch: strided views would give wrong rows
+        if count is None and (mask.dtype.itemsize != 8 or mask.dim() != 2 or mask.shape[1] != self.words + 1
+                              or not mask.is_contiguous()):
+            raise RuntimeError("pack_accepted: records must be contiguous int64 (n, words + 1)")
+        if count is not None and (count.dtype.itemsize != 4 or not count.is_contiguous()
+                                  or mask.dtype.itemsize != 8 or tuple(mask.shape) != (n, self.words)
+                                  or not mask.is_contiguous()):
+            raise RuntimeError(f"pack_accepted: count must be contiguous int32 (n,) and mask contiguous "
+                               f"int64 (n, {self.words})")
         cap = int(out.shape[0]) - 1
         width = 1 + self.words + (3 if c is not None else 0)
         if out.dtype.itemsize != 8 or out.shape[1] != width or not out.is_contiguous():

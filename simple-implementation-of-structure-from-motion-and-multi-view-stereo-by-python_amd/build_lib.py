@@ -61,8 +61,17 @@ def build(force=False, verbose=False, stamps=False, asan=False):
     bad = [f for f, p in zip(SOURCES, procs) if p.wait() != 0]
     if bad:
         raise subprocess.CalledProcessError(1, f"hipcc {bad}")
-    link = [c for c in cmd if c not in ("-mllvm", "-amdgpu-atomic-optimizer-strategy=None")] + \
-        ["-shared", "-o", out + ".tmp"] + objs
+    # the link takes the compile options minus the "-mllvm X" pairs (removed
+    # pairwise: a bare X left behind would be an unknown argument)
+    link = []
+    k = 0
+    while k < len(cmd):
+        if cmd[k] == "-mllvm":
+            k += 2
+            continue
+        link.append(cmd[k])
+        k += 1
+    link += ["-shared", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(link), file=sys.stderr)
     subprocess.check_call(link, cwd=CSRC)

@@ -345,20 +345,33 @@ struct mvs_ctx {
     // apply (disabled, or more than 2^31 elements).  One row of 16 pixels
     // past the end: k_score_tab stages a tile's rows whole (16 pixels x VP),
     // also where the last tile column runs past W
+    // Memory: (H W + 16) VP elements per wid, 10 B each at V <= 64 (S_b int16
+    // + w binary64) or 6 B at V > 64 (S_b + D int32): 147 MB per wid at
+    // dinoRing, 3.2 GB at 256 x 1920 x 1080.  A scene past tab_limit elements (2^31;
+    // env MVS_TAB_LIMIT lowers it, for tests) or whose tables cannot be
+    // allocated is scored with the in-kernel moments instead (same results).
+    int64_t tab_limit = (int64_t)1 << 31;
     bool ensure_moments(int wid, hipStream_t s) {
         if (tab_mode == 1) return false;
         const int64_t elems = ((int64_t)H * W + 16) * moments_vp();
-        if (elems >= ((int64_t)1 << 31)) return false;
+        if (elems >= tab_limit) return false;
         if (!mom_ok[wid]) {
-            mom_sb[wid].alloc((size_t)elems);
-            HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
-            if (moments_dtab(V)) {
-                mom_d[wid].alloc((size_t)elems);
-                HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
-            } else {
-                mom_w[wid].alloc((size_t)elems);
-                HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
+            try {
+                mom_sb[wid].alloc((size_t)elems);
+                if (moments_dtab(V)) mom_d[wid].alloc((size_t)elems);
+                else mom_w[wid].alloc((size_t)elems);
+            } catch (const Fail&) {
+                mom_sb[wid].release();
+                mom_d[wid].release();
+                mom_w[wid].release();
+                (void)hipGetLastError();   // the failed hipMalloc's error is not this call's
+                return false;
             }
+            HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
+            if (moments_dtab(V))
+                HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
+            else
+                HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
             const MomentsDev m = moments(wid);
             if (mvs_launch_moments(&sc, &m, s) != 0) throw Fail{MVS_E_HIP, "moments launch failed"};
             mom_ok[wid] = true;
@@ -1372,6 +1385,7 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
             else if (!std::strcmp(km, "tab")) ctx->tab_mode = 2;   // tiled, tables at every V
         }
         if (const char* sw = std::getenv("MVS_SCORER_WGS")) ctx->scorer_wgs = std::max(0, std::atoi(sw));
+        if (const char* tl = std::getenv("MVS_TAB_LIMIT")) ctx->tab_limit = std::max<int64_t>(1, std::atoll(tl));
         return 0;
     });
     if (rc != 0) {

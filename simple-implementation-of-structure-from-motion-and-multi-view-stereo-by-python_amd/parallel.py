@@ -151,16 +151,17 @@ class PointsExchange:
 
     def check(self, b=None):
         """Wait for buffer b's exchange (default: the last posted) and raise if
-        any rank's pack failed (header -1) or accepted more candidates than the
-        capacity; -> the (world, cap + 1, width) gathered block."""
+        any rank's header is not a row count (a buffer no pack wrote) or
+        accepted more candidates than the capacity; -> the (world, cap + 1,
+        width) gathered block."""
         b = (self.posted - 1) & 1 if b is None else b
         if self.done[b] is not None:
             self.done[b].synchronize()
         blk = self.blocks(b)
         acc = blk[:, 0, 0].tolist()
         if min(acc) < 0:
-            raise RuntimeError(f"PointsExchange: the device pack of rank(s) "
-                               f"{[r for r, a in enumerate(acc) if a < 0]} failed (look-back gave up)")
+            raise RuntimeError(f"PointsExchange: rank(s) {[r for r, a in enumerate(acc) if a < 0]} "
+                               f"sent a negative row count (corrupt buffer)")
         if max(acc) > self.cap:
             raise RuntimeError(f"PointsExchange capacity {self.cap} < accepted {max(acc)}")
         return blk

@@ -283,12 +283,13 @@ def _smooth_ring(pkg, V, H=96, W=128):
     return rgb, K, R, t
 
 
-@pytest.mark.parametrize("mode", ["", "tab"])
+@pytest.mark.parametrize("mode", ["mma", ""])
 @pytest.mark.parametrize("V,wid", [(68, 5), (100, 3), (256, 3), (100, 1), (132, 2), (200, 4)])
 def test_view_groups_wid_and_partial_group(pkg, orc, V, wid, mode):
     """The view-group path k_score_mma_v (V > 64) with a 4-view last group
-    (V = 68), every window size; in-kernel moments (default) and the D tables
-    (MVS_SCORE_KERNEL=tab)."""
+    (V = 68), every window size; the default reads S_b and D from the scene's
+    tables, MVS_SCORE_KERNEL=mma forces the in-kernel moments (the path a
+    scene past the tables' size cutoff takes)."""
     import os
     H, W = 96, 128
     rgb, K, R, t = _smooth_ring(pkg, V, H, W)
@@ -307,6 +308,37 @@ def test_view_groups_wid_and_partial_group(pkg, orc, V, wid, mode):
             for g, e in zip(got[:3], exp[:3]):
                 assert np.array_equal(g, e)
             np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+
+
+@pytest.mark.parametrize("V", [48, 100])
+def test_table_cutoff_falls_back_to_in_kernel_moments(pkg, orc, dino, V):
+    """A scene whose window-moment tables would exceed the element cutoff
+    (2^31; MVS_TAB_LIMIT lowers it here) is scored with the in-kernel
+    moments -- k_score_mma at V <= 64, k_score_mma_v without tables above --
+    and stays bit-exact against the oracle."""
+    import os
+    if V == 48:
+        rgb, K, R, t = dino
+        H, W = rgb.shape[1:3]
+    else:
+        H, W = 96, 128
+        rgb, K, R, t = _smooth_ring(pkg, V, H, W)
+    os.environ["MVS_TAB_LIMIT"] = "1000"
+    try:
+        cx = pkg.MvsContext(rgb, K, R, t)
+    finally:
+        os.environ.pop("MVS_TAB_LIMIT", None)
+    with cx:
+        c, ref = pkg.synthetic.candidates(20000, K, R, t, W=W, H=H, seed=7)
+        cx.kernel_timing(True)
+        got = cx.score(c, ref, 0.6, 5)
+        cx.kernel_timing(False)
+        assert cx.timed_kernel() == ("k_score_mma" if V <= 64 else "k_score_mma_v")
+        exp = orc.Scene(rgb, K, R, t).score_batch(c, ref, 0.6, 5, nthreads=8)
+        for g, e in zip(got[:3], exp[:3]):
+            assert np.array_equal(g, e)
+        np.testing.assert_allclose(got[3], exp[3], rtol=0, atol=AVG_TOL)
+        assert (got[2] >= 3).sum() > (100 if V <= 64 else 0)
 
 
 def test_view_groups_threshold_on_reference_value(pkg, orc):
