@@ -271,9 +271,11 @@ def launch_ranks(nranks):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    # the ranks' arguments travel in the environment: torch.distributed.run
+    # would take some of them (e.g. --n) as abbreviations of its own options
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
-    env = dict(os.environ, MVS_BENCH_LAUNCHED="1")
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    env = dict(os.environ, MVS_BENCH_ARGV=json.dumps(sys.argv[1:]))
     line = None
     with subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env) as p:
         for ln in p.stdout:
@@ -315,7 +317,8 @@ def main():
                     help="score into the three output arrays (mask, count, avg) instead of one record per candidate")
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
                     help="headline scene (ring256: config 4 as the headline, for profiling)")
-    a = ap.parse_args()
+    argv = json.loads(os.environ["MVS_BENCH_ARGV"]) if "MVS_BENCH_ARGV" in os.environ else None
+    a = ap.parse_args(argv)
     if a.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
