@@ -2272,8 +2272,21 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
 // Measurement only (bench.py exchange.overlap_proxy): a copy of n 16-B pieces
 // by a fixed number of workgroups -- the footprint of an RCCL all-gather's
 // kernel (a few CUs streaming bytes) -- to run beside the scoring kernels.
+// Eight pieces per thread in flight, as a collective's copy loop keeps them
+// (one at a time makes the copy latency-bound: 3x slower beside the scorer,
+// profiles/r05/r5a_timeline.txt).
 __global__ __launch_bounds__(256) void k_proxy_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+    constexpr int U = 8;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += U * stride) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * stride < n) v[u] = src[i0 + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * stride < n) dst[i0 + u * stride] = v[u];
+    }
 }
 
 // reconstruct_from_Q (MVS2.py:159-173): an accepted patch is appended under

@@ -105,18 +105,33 @@ def main():
         src = torch.zeros(recv // 8, dtype=torch.int64, device=dev)
         dst = torch.empty_like(src)
 
+        # "pipe": the pack runs on the comm stream too (before the copy), on
+        # the sweep's records of the previous step (two record buffers)
+        pipe = "pipe" in var
+        recs = [sw["rec"], torch.empty_like(sw["rec"])]
+        done = [None, None]
+
         def run(k, with_proxy, proxy_only=False):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(k):
+            for st in range(k):
+                rec = recs[st & 1] if pipe else sw["rec"]
                 if not proxy_only:
-                    ctx.score_device_rec(sw["c"], sw["ref"], sw["xy"], sw["rec"], 0.7, 5, stream=stream.cuda_stream)
-                    ctx.pack_accepted(0, None, sw["rec"], vlb, out, stream=stream.cuda_stream, c=sw["c"])
-                if with_proxy:
+                    if pipe and done[st & 1] is not None:
+                        stream.wait_event(done[st & 1])     # the pack two steps back has read rec
+                    ctx.score_device_rec(sw["c"], sw["ref"], sw["xy"], rec, 0.7, 5, stream=stream.cuda_stream)
+                    if not pipe:
+                        ctx.pack_accepted(0, None, rec, vlb, out, stream=stream.cuda_stream, c=sw["c"])
+                if with_proxy or pipe:
                     ev = torch.cuda.Event()
                     ev.record(stream)
                     comm.wait_event(ev)
-                    pkg._lib.proxy_copy(dst, src, recv, a.workgroups, comm.cuda_stream)
+                    if pipe and not proxy_only:
+                        ctx.pack_accepted(0, None, rec, vlb, out, stream=comm.cuda_stream, c=sw["c"])
+                        done[st & 1] = torch.cuda.Event()
+                        done[st & 1].record(comm)
+                    if with_proxy:
+                        pkg._lib.proxy_copy(dst, src, recv, a.workgroups, comm.cuda_stream)
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) / k * 1e6
 
