@@ -393,6 +393,19 @@ struct mvs_ctx {
     // waits for the previous one (an event on the stream that used it last).
     hipEvent_t scratch_ev = nullptr;
     hipStream_t scratch_s = nullptr;
+    // the same for the exchange pack's status words and ticket
+    struct StreamOrder {
+        hipEvent_t ev = nullptr;
+        hipStream_t s = nullptr;
+        void acquire(hipStream_t cur) {
+            if (s && s != cur) HIPCHK(hipStreamWaitEvent(cur, ev, 0));
+        }
+        void release(hipStream_t cur) {
+            if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(ev, cur));
+            s = cur;
+        }
+    } pack_order;
     std::string err;
     void scratch_acquire(hipStream_t s) {
         if (scratch_s && scratch_s != s) HIPCHK(hipStreamWaitEvent(s, scratch_ev, 0));
@@ -1400,10 +1413,12 @@ void mvs_ctx_destroy(mvs_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->scratch_ev) (void)hipEventSynchronize(ctx->scratch_ev);
+    if (ctx->pack_order.ev) (void)hipEventSynchronize(ctx->pack_order.ev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
     if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
+    if (ctx->pack_order.ev) (void)hipEventDestroy(ctx->pack_order.ev);
     delete ctx;
 }
 
@@ -1506,7 +1521,10 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
         return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
     return guarded(ctx, [&]() {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        ctx->scratch_acquire(s);
+        // the pack's own scratch (status words, ticket): ordered against the
+        // previous pack only, so that a pack on a communication stream does
+        // not order the next sweep's scoring behind it
+        ctx->pack_order.acquire(s);
         const uint64_t* st_before = ctx->p_status.p;
         ctx->p_status.ensure(std::max<int64_t>((n + MVS_ACC_CHUNK - 1) / MVS_ACC_CHUNK, 1));
         if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used
@@ -1514,14 +1532,14 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
             ctx->p_epoch = 0;
         }
         if (!ctx->p_err.p) {
-            ctx->p_err.ensure(1);
-            HIPCHK(hipMemsetAsync(ctx->p_err.p, 0, sizeof(int32_t), s));
+            ctx->p_err.ensure(2);   // [0] slow-path chunks, [1] the chunk ticket (k_acc_pack returns it to 0)
+            HIPCHK(hipMemsetAsync(ctx->p_err.p, 0, 2 * sizeof(int32_t), s));
         }
         ctx->p_epoch = ctx->p_epoch % ((1ull << 30) - 1) + 1;   // 1 .. 2^30 - 1
         if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, d_c, ctx->words(), vlb, cap, ctx->p_status.p,
                                      ctx->p_epoch, ctx->p_err.p, ctx->pack_debug, d_out, s) != 0)
             throw Fail{MVS_E_HIP, "pack launch failed"};
-        ctx->scratch_release(s);
+        ctx->pack_order.release(s);
         return 0;
     });
 }

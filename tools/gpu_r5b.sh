@@ -6,6 +6,8 @@ export TMPDIR=/tmp
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 T=${TAG:-r5b}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -k "pack or exchange or bench_ranks or records" > gpurun_out/${T}_pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/${T}_pytest.log; grep "pack_accepted (" gpurun_out/${T}_pytest.log; [ $rc -ne 0 ] && { grep -B5 -A40 "FAILED\|Error" gpurun_out/${T}_pytest.log | head -80; exit $rc; }
 timeout -k 10 120 tools/ubench/bin_atomics > gpurun_out/${T}_bin_atomics.log 2>&1 || { cat gpurun_out/${T}_bin_atomics.log; exit 1; }
 cat gpurun_out/${T}_bin_atomics.log
 for args in "base cumask pipe cumask+pipe --free 16" "cumask cumask+pipe --free 32" "cumask cumask+pipe --free 16 --mask-order spread" "cumask --free 16 --mask-order lo"; do
