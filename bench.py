@@ -68,19 +68,23 @@ def logical_bytes(V, wid):
     return V * (2 * wid + 1) ** 2 + 32 + 8 * ((V + 63) // 64) + 16
 
 
-def score(cx, sw, wid, thr, stream):
+def score(cx, sw, wid, thr, stream, rec=None):
     """One sweep's photo test: records (mvs_score_device_rec, one 16-B store per
-    candidate at V <= 64) unless --soa asked for the three-array outputs."""
+    candidate at V <= 64; `rec` overrides the buffer) unless --soa asked for
+    the three-array outputs."""
     if sw["rec"] is not None:
-        cx.score_device_rec(sw["c"], sw["ref"], sw["xy"], sw["rec"], thr, wid, stream=stream.cuda_stream)
+        cx.score_device_rec(sw["c"], sw["ref"], sw["xy"], sw["rec"] if rec is None else rec, thr, wid,
+                            stream=stream.cuda_stream)
     else:
         cx.score_device(sw["c"], sw["ref"], sw["xy"], sw["mask"], sw["count"], sw["avg"], thr, wid,
                         stream=stream.cuda_stream)
 
 
-def pack_src(sw):
+def pack_src(sw, rec=None):
     """(count, mask) arguments of the pack: (None, records) or the arrays."""
-    return (None, sw["rec"]) if sw["rec"] is not None else (sw["count"], sw["mask"])
+    if sw["rec"] is not None:
+        return None, (sw["rec"] if rec is None else rec)
+    return sw["count"], sw["mask"]
 
 
 def host_outputs(sw, m=None):
@@ -315,6 +319,12 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="skip the exchange overlap proxy")
     ap.add_argument("--soa", action="store_true",
                     help="score into the three output arrays (mask, count, avg) instead of one record per candidate")
+    ap.add_argument("--comm-cus", type=int, default=16,
+                    help="N > 1 (and the N = 1 with-pack baseline): CUs left out of the scoring stream's "
+                         "CU mask for the exchange's pack and all-gather (0: no mask)")
+    ap.add_argument("--pack-on-scoring-stream", action="store_true",
+                    help="N > 1: pack on the scoring stream (default: on the exchange's stream, overlapping "
+                         "the next sweep)")
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
                     help="headline scene (ring256: config 4 as the headline, for profiling)")
     argv = json.loads(os.environ["MVS_BENCH_ARGV"]) if "MVS_BENCH_ARGV" in os.environ else None
@@ -389,24 +399,35 @@ def main():
                 "rec": None if a.soa else torch.empty((n, (ctx_V + 63) // 64 + 1), dtype=torch.int64, device=dev),
                 "avg": torch.empty(n, dtype=torch.float64, device=dev)}
 
-    def timed(cx, sw, wid, steps, warmup, exchange=True, rebuild=False):
-        """steps timed sweeps -> (wall s (max over ranks), kernel ms per launch,
-        score-call ms, records exchanged in the last step)."""
+    def timed(cx, sw, wid, steps, warmup, exchange=True, rebuild=False, st=None):
+        """steps timed sweeps on stream st (default: the scoring stream) ->
+        (wall s (max over ranks), kernel ms per launch, score-call ms, records
+        exchanged in the last step)."""
         got = {"n": 0}
+        st = st or stream
+        ex = sw.get("exch") if exchange else None
 
         def step(evs=None):
+            rec = None
+            if ex is not None and ex.pack_on_comm and sw["rec"] is not None:
+                # two record buffers: sweep k+1 scores into one while the comm
+                # stream packs sweep k's from the other
+                b = ex.posted & 1
+                rec = sw["recs"][b]
+                if ex.consumed(b) is not None:
+                    st.wait_event(ex.consumed(b))
             if evs is not None:
-                evs[0].record(stream)
+                evs[0].record(st)
             if rebuild:
-                cx.rebuild(stream=stream.cuda_stream)
-            score(cx, sw, wid, a.thr, stream)
+                cx.rebuild(stream=st.cuda_stream)
+            score(cx, sw, wid, a.thr, st, rec)
             if evs is not None:
-                evs[1].record(stream)
-            if exchange and "exch" in sw:
+                evs[1].record(st)
+            if ex is not None:
                 # pack (device, no host sync) + at N > 1 the all-gather on the
                 # exchange's own stream, overlapping the next sweep
                 # (parallel.PointsExchange); at N = 1 the pack alone
-                sw["exch"].post(sw["off"], *pack_src(sw), vlb, stream=stream, c=sw["c"])
+                ex.post(sw["off"], *pack_src(sw, rec), vlb, stream=st, c=sw["c"])
 
         for _ in range(warmup):
             step()
@@ -431,8 +452,8 @@ def main():
         if kl != len(timed_steps) or kt <= 0.0:
             raise RuntimeError(f"kernel timing recorded {kl} launches / {kt} ms for {len(timed_steps)} timed steps")
         pms = sum(e0.elapsed_time(e1) for e0, e1 in evs.values()) / len(evs)
-        if exchange and "exch" in sw:
-            got["n"] = int(sum(sw["exch"].accepted()))    # every rank's rows arrived, none over capacity / failed
+        if ex is not None:
+            got["n"] = int(sum(ex.accepted()))    # every rank's rows arrived, none over capacity / failed
         if world > 1:
             tt = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -441,6 +462,20 @@ def main():
 
     sw = sweep_inputs(V, K, R, t, W, H, a.n, a.strong)
     n = sw["n"]
+    if sw["rec"] is not None:
+        sw["recs"] = [sw["rec"], torch.empty_like(sw["rec"])]
+    # the multi-GPU step's layout: scoring on a CU-masked stream
+    # (all CUs but --comm-cus), the scorer's grid at two workgroups per kept
+    # CU, and the pack + all-gather on the exchange's stream, where they find
+    # the free CUs instead of queueing behind the persistent scorer
+    mstream, kept = stream, None
+    if a.comm_cus > 0 and (world > 1 or rank == 0):
+        mstream, kept = par.cu_masked_stream(dev, a.comm_cus)
+
+    def masked(on):
+        ctx.set_scorer_grid(2 * kept if on and kept else 0)
+
+    pack_on_comm = not a.pack_on_scoring_stream
     if world > 1:
         # exchange capacity: this sweep's accepted count (one untimed score),
         # the maximum over ranks plus a margin (rows of every rank are equal-sized)
@@ -449,9 +484,11 @@ def main():
         kk = torch.tensor([int((host_outputs(sw)[1] >= vlb).sum())], dtype=torch.int64, device=dev)
         dist.all_reduce(kk, op=dist.ReduceOp.MAX)
         cap = int(kk.item()) + int(kk.item()) // 16 + 256
-        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap, dev)
+        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap, dev, pack_on_comm=pack_on_comm)
+        masked(True)
     total_n = a.n if a.strong else a.n * world
-    dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup)
+    dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream if world > 1 else stream)
+    masked(False)
     value = total_n * a.steps / dt
     accepted = int((host_outputs(sw)[1] >= vlb).sum())
     acc_ranks = [accepted]
@@ -466,13 +503,18 @@ def main():
         # score + the 40-B point pack (PointsExchange at world 1), so that a
         # 1 -> N comparison can also be made on the same device work
         cap1 = accepted + accepted // 16 + 256
-        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap1, dev)
-        pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup)
+        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap1, dev, pack_on_comm=pack_on_comm)
+        masked(True)
+        pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream)
+        masked(False)
         del sw["exch"]
         if packed != accepted:
             raise RuntimeError(f"N = 1 pack: {packed} rows != {accepted} accepted")
         scaling_base = {"step_ms_with_pack": pdt / a.steps * 1e3, "value_with_pack": n * a.steps / pdt,
                         "step_ms_score_only": dt / a.steps * 1e3,
+                        "layout": (f"scoring on {kept} of {kept + a.comm_cus} CUs (CU-masked stream), " if kept else
+                                   "scoring on every CU, ") +
+                                  ("pack on the exchange's stream" if pack_on_comm else "pack on the scoring stream"),
                         "note": "`value` at N = 1 is the scoring step alone (no exchange exists on one GPU); "
                                 "at N > 1 a step adds the 40-B point pack and the all-gather (overlapped "
                                 "with the next sweep). value_with_pack is the N = 1 step with the pack"}

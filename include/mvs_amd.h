@@ -130,6 +130,12 @@ int64_t mvs_pack_fallbacks(mvs_ctx* ctx);
  * chunk -mode (2,048 candidates each) down the slow path at once, 0 restores
  * the default. */
 int mvs_pack_debug(mvs_ctx* ctx, int64_t mode);
+/* The persistent tiled scorers' grid: `workgroups` > 0 holds them to that
+ * many workgroups (at two per CU, the CUs of a CU-masked scoring stream), 0
+ * restores the default (every CU, twice).  Multi-GPU steps score on a stream
+ * whose CU mask leaves a few CUs to the exchange's pack and RCCL's kernels
+ * (parallel.cu_masked_stream); no reference counterpart. */
+int mvs_set_scorer_grid(mvs_ctx* ctx, int workgroups);
 /* Kernel timing (measurement only): while enabled, every enable-th scoring
  * call (enable = 1: every call) records a HIP event pair on its stream
  * immediately around the dominant scoring kernel (k_score_mma / k_score_mma_v

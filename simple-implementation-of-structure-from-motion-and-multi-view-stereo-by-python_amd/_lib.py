@@ -38,6 +38,7 @@ SIGNATURES = [
     ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
                                          ctypes.c_int64, _vp, _vp]),
     ("mvs_pack_debug", ctypes.c_int, [_vp, ctypes.c_int64]),
+    ("mvs_set_scorer_grid", ctypes.c_int, [_vp, ctypes.c_int]),
     ("mvs_pack_fallbacks", ctypes.c_int64, [_vp]),
     ("mvs_proxy_copy", ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp]),
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
@@ -353,6 +354,11 @@ class MvsContext:
                                       int(vlb), cap, out.data_ptr(),
                                       stream if stream is not None else None)
         check(rc, self._h, "mvs_pack_accepted")
+
+    def set_scorer_grid(self, workgroups=0):
+        """Hold the persistent scorers to `workgroups` workgroups (0: default,
+        two per CU): the grid for a CU-masked scoring stream."""
+        check(load().mvs_set_scorer_grid(self._h, int(workgroups)), self._h, "mvs_set_scorer_grid")
 
     def pack_debug(self, mode=0):
         """Tests only: the pack's look-back spin limit (mode > 0) or the slow

@@ -1564,6 +1564,13 @@ int64_t mvs_pack_fallbacks(mvs_ctx* ctx) {
     return rc ? rc : h;
 }
 
+int mvs_set_scorer_grid(mvs_ctx* ctx, int workgroups) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (workgroups < 0) return set_err(ctx, Fail{MVS_E_ARG, "workgroups must be >= 0"});
+    ctx->scorer_wgs = workgroups;
+    return 0;
+}
+
 int mvs_pack_debug(mvs_ctx* ctx, int64_t mode) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
     ctx->pack_debug = mode;

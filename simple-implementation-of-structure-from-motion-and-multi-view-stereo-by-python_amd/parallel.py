@@ -25,6 +25,33 @@ import torch
 import torch.distributed as dist
 
 
+def cu_masked_stream(device, free_cus):
+    """A stream of `device` whose kernels run on all CUs but `free_cus` of
+    them (hipExtStreamCreateWithCUMask; bit k of the mask = CU k as HIP
+    numbers them, the highest free_cus left out), as a torch ExternalStream,
+    and the number of CUs it keeps.  The multi-GPU step scores on such a
+    stream with the scorer's grid at two workgroups per kept CU
+    (MvsContext.set_scorer_grid), so that the exchange's pack and RCCL's
+    all-gather kernels find CUs of their own instead of waiting for the
+    persistent scorer's workgroups (bench.py)."""
+    import ctypes
+    dev = torch.device(device)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    keep = max(ncu - int(free_cus), 1)
+    words = []
+    for w in range((ncu + 31) // 32):
+        lo, hi = 32 * w, min(32 * w + 32, keep)
+        words.append(((1 << (hi - lo)) - 1) if hi > lo else 0)
+    hip = ctypes.CDLL("libamdhip64.so")
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), arr)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(handle.value, device=dev), keep
+
+
 def shard_range(n, rank, world):
     """Contiguous slice [begin, end) of n items for `rank` (sizes differ by <= 1)."""
     base, extra = divmod(n, world)
@@ -78,9 +105,14 @@ class PointsExchange:
     ctx = the rank's MvsContext (its pack kernel); on CPU tensors (gloo) the
     torch reference pack is used and the all-gather is synchronous."""
 
-    def __init__(self, ctx, words, cap, device, group=None, points=True):
+    def __init__(self, ctx, words, cap, device, group=None, points=True, pack_on_comm=False):
         self.ctx, self.words, self.cap, self.group = ctx, words, int(cap), group
         self.points = bool(points)
+        # pack_on_comm: the pack runs on the communication stream as well (after
+        # the scoring stream's sweep), overlapping the next sweep's scoring;
+        # the caller then leaves the sweep's outputs alone until consumed(b)
+        self.pack_on_comm = bool(pack_on_comm)
+        self.read = [None, None]
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.width = points_width(words, self.points)
         self.device = torch.device(device)
@@ -88,7 +120,8 @@ class PointsExchange:
         self.send = [torch.zeros((self.cap + 1, self.width), dtype=torch.int64, device=device) for _ in range(2)]
         self.recv = [torch.zeros((self.world * (self.cap + 1), self.width), dtype=torch.int64, device=device)
                      for _ in range(2)]
-        self.comm = torch.cuda.Stream(self.device) if cuda and self.world > 1 else None
+        self.comm = (torch.cuda.Stream(self.device) if cuda and (self.world > 1 or self.pack_on_comm)
+                     else None)
         self.done = [None, None]
         self.posted = 0
 
@@ -107,6 +140,24 @@ class PointsExchange:
                 # the C-ABI reads stream 0 as "the library's own stream": the pack
                 # would not be ordered with this stream's events
                 raise RuntimeError("PointsExchange.post needs a non-default stream")
+            if self.pack_on_comm:
+                scored = torch.cuda.Event()
+                scored.record(cur)
+                self.comm.wait_event(scored)          # send[b]'s last gather ran on comm itself
+                self.ctx.pack_accepted(offset, count, mask, vlb, self.send[b], stream=self.comm.cuda_stream, c=cc)
+                rd = torch.cuda.Event()
+                rd.record(self.comm)
+                self.read[b] = rd
+                if self.world == 1:
+                    self.done[b] = rd
+                    return b
+                with torch.cuda.stream(self.comm):
+                    work = dist.all_gather_into_tensor(self.recv[b], self.send[b], group=self.group, async_op=True)
+                    work.wait()
+                    ev = torch.cuda.Event()
+                    ev.record(self.comm)
+                self.done[b] = ev
+                return b
             if self.done[b] is not None:
                 cur.wait_event(self.done[b])          # the all-gather two sweeps back has read send[b]
             self.ctx.pack_accepted(offset, count, mask, vlb, self.send[b], stream=cur.cuda_stream, c=cc)
@@ -127,6 +178,11 @@ class PointsExchange:
         if self.world > 1:
             dist.all_gather_into_tensor(self.recv[b], self.send[b], group=self.group)
         return b
+
+    def consumed(self, b):
+        """pack_on_comm: the event after which the sweep posted into buffer b
+        no longer reads its outputs (None before the first post)."""
+        return self.read[b]
 
     def blocks(self, b):
         """(world, cap + 1, width) view of buffer b's gathered rows (device);
