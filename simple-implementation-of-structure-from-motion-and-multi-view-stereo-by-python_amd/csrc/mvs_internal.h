@@ -118,6 +118,10 @@ struct TiledArgs {
     // workgroups of the persistent scorer (0: its default, every CU; fewer
     // leave CUs free for a kernel that runs beside it, e.g. RCCL's)
     int grid;
+    // implicit items (k_score_tab, dense batches; set by the launcher): item
+    // k < ntiles is (tile k, chunk 0) -- tile order without k_item_scan --
+    // and k_bin appends the further chunks (tile, j >= 1) to segment 1
+    int implicit;
 };
 
 // Per-scene window moments of the tiled scorers, one table pair per window

@@ -343,6 +343,10 @@ __device__ unsigned long long g_stamps[4096 * 16];
 #endif
 
 constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
+#ifndef MVS_IMPLICIT_MEAN
+#define MVS_IMPLICIT_MEAN 64   // A/B switch (a huge value keeps k_item_scan everywhere)
+#endif
+constexpr int64_t kImplicitMean = MVS_IMPLICIT_MEAN;
 constexpr int kMmaGrid = 256;         // the scorers' workgroups: one per CU; the queue balances
 
 // The work items in tile order: one workgroup reads every tile's count, scans
@@ -443,6 +447,9 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             lr[k] = atomicAdd(&hist[tile], 1);
         } else {
             lr[k] = atomicAdd(&t.tile_count[tile * kTcStride], 1);
+            // implicit items: the candidate that opens chunk j >= 1 appends it
+            if (t.implicit && lr[k] > 0 && lr[k] < t.cap && lr[k] % t.chunk == 0)
+                t.items[t.item_seg + atomicAdd(&t.n_items[32], 1)] = make_int4(tile, lr[k] / t.chunk, 0, 0);
         }
     }
     STAMP(t1);
@@ -456,6 +463,18 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             const int b = threadIdx.x + j * kBinBlock;
             const int c = b < t.ntiles ? hist[b] : 0;
             bs[j] = c ? atomicAdd(&t.tile_count[b * kTcStride], c) : 0;
+        }
+        if (t.implicit) {
+            // implicit items: the workgroup whose share of a tile's bucket
+            // holds the first entry of chunk j >= 1 (below cap) appends (tile, j)
+#pragma unroll
+            for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
+                const int b = threadIdx.x + j * kBinBlock;
+                const int c = b < t.ntiles ? hist[b] : 0;
+                const int end = min(bs[j] + c, t.cap);
+                for (int q = max((bs[j] + t.chunk - 1) / t.chunk, 1); c > 0 && q * t.chunk < end; ++q)
+                    t.items[t.item_seg + atomicAdd(&t.n_items[32], 1)] = make_int4(b, q, 0, 0);
+            }
         }
 #pragma unroll
         for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
@@ -2500,13 +2519,19 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);
+    // k_score_tab on a dense batch (>= kImplicitMean candidates per tile on
+    // average: every tile holds some, so an empty item is rare) takes the
+    // tiles themselves as its items, in tile order, and needs no k_item_scan
+    TiledArgs tv = *t;
+    tv.implicit = (!grouped && mt && a->n >= (int64_t)kImplicitMean * t->ntiles) ? 1 : 0;
     if (t->ntiles <= kBinLdsTiles)
-        hipLaunchKernelGGL(k_bin<true>, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, *t, WID);
+        hipLaunchKernelGGL(k_bin<true>, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, tv, WID);
     else
-        hipLaunchKernelGGL(k_bin<false>, dim3(nbin), dim3(kBinBlock), 0, s, *sc, *a, *t, WID);
+        hipLaunchKernelGGL(k_bin<false>, dim3(nbin), dim3(kBinBlock), 0, s, *sc, *a, tv, WID);
     // the work items in tile order (the scorers' workgroups in flight then
     // share image rows -- and at V > 64 table rows -- in L2)
-    hipLaunchKernelGGL(k_item_scan, dim3(1), dim3(kScanThreads), 0, s, *t);
+    if (!tv.implicit) hipLaunchKernelGGL(k_item_scan, dim3(1), dim3(kScanThreads), 0, s, tv);
+    t = &tv;
     int rc = 0;
     {
         TimedLaunch tl(s, ev0, ev1);

@@ -239,7 +239,10 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     const float tqf = (float)(a.thr / kn);
     ItemMap im;
     im.load(t);
-    const int n_units = im.total();
+    // implicit items: k < ntiles is (tile k, chunk 0), then segment 1's
+    // further chunks (k_bin); else k_item_scan's list
+    const bool implicit = t.implicit != 0;
+    const int n_units = implicit ? t.ntiles + t.n_items[32] : im.total();
     int32_t* head = t.head;
     const int16_t* __restrict__ tsb = mt.sb;
     const double* __restrict__ tw = mt.w;
@@ -317,7 +320,11 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     // vector loads (a lane-dependent-looking address): their wait is the
     // in-order vmcnt at the round's end, not lgkmcnt(0) in front of every LDS
     // read of the round
-    auto item_v = [&](int v) -> int2 { return *(const int2*)(items + opaque(im.slot(v))); };
+    auto item_v = [&](int v) -> int2 {
+        // the load is issued either way (its wait stays the round end's vmcnt)
+        const int2 ld = *(const int2*)(items + opaque(implicit ? t.item_seg + max(v - t.ntiles, 0) : im.slot(v)));
+        return implicit && v < t.ntiles ? make_int2(v, 0) : ld;
+    };
     auto count_v = [&](int tile) -> int { return t.tile_count[opaque(tile * kTcStride)]; };
     // the item pipeline: while item k is scored, item k+1's region and list
     // (DB) and its tile's count, item k+2's (tile, chunk) and thread 0's claim

@@ -6,8 +6,8 @@ export TMPDIR=/tmp
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 T=${TAG:-r5b}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -k "pack or exchange or bench_ranks or records" > gpurun_out/${T}_pytest.log 2>&1
-rc=$?; tail -2 gpurun_out/${T}_pytest.log; grep "pack_accepted (" gpurun_out/${T}_pytest.log; [ $rc -ne 0 ] && { grep -B5 -A40 "FAILED\|Error" gpurun_out/${T}_pytest.log | head -80; exit $rc; }
+[ -z "$FROM_C" ] && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -k "pack or exchange or bench_ranks or records" > gpurun_out/${T}_pytest.log 2>&1
+rc=$?; [ -z "$FROM_C" ] && { tail -2 gpurun_out/${T}_pytest.log; grep "pack_accepted (" gpurun_out/${T}_pytest.log; }; [ -z "$FROM_C" ] && [ $rc -ne 0 ] && { grep -B5 -A40 "FAILED\|Error" gpurun_out/${T}_pytest.log | head -80; exit $rc; }
 timeout -k 10 120 tools/ubench/bin_atomics > gpurun_out/${T}_bin_atomics.log 2>&1 || { cat gpurun_out/${T}_bin_atomics.log; exit 1; }
 cat gpurun_out/${T}_bin_atomics.log
 for args in "base cumask pipe cumask+pipe --free 16" "cumask cumask+pipe --free 32" "cumask cumask+pipe --free 16 --mask-order spread" "cumask --free 16 --mask-order lo"; do
@@ -22,3 +22,4 @@ for v in "cumask+pipe" "base"; do
   python tools/overlap_timeline.py gpurun_out/${T}_${v}_kernel_trace.csv 60 45 > gpurun_out/${T}_${v}_timeline.txt
   echo "== trace $v"; cat gpurun_out/${T}_${v}_timeline.txt | cut -c1-110
 done
+timeout -k 10 120 rocprofv3 -L > gpurun_out/${T}_counters.txt 2>&1; grep -E "^\s*(TA_|TD_|TCP_)" gpurun_out/${T}_counters.txt | head -80 > gpurun_out/${T}_counters_ta.txt; wc -l gpurun_out/${T}_counters.txt

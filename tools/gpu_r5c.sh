@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-5 iteration: GPU tests, the headline-only bench (twice, + rocprof
+# kernel stats), then the probes of gpu_r5b.sh (bin_atomics, overlap probe,
+# traces, counter list).  TAG names the outputs; NO_PROBES skips the probes.
+export TMPDIR=/tmp
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+T=${TAG:-r5c}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${T}_pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/${T}_pytest.log; grep "pack_accepted (" gpurun_out/${T}_pytest.log
+if [ $rc -ne 0 ]; then grep -B5 -A40 "FAILED\|Error" gpurun_out/${T}_pytest.log | head -80; [ $rc -ne 1 ] && exit $rc; fi
+B="--no-stage --no-ring --secondary-wid 0 --steps 100 --no-cpu-baseline --no-overlap ${BENCH_ARGS}"
+for rep in 1 2; do
+  timeout -k 10 300 python bench.py $B > gpurun_out/${T}_b$rep.json 2>gpurun_out/${T}_b.err || { tail -5 gpurun_out/${T}_b.err; exit 1; }
+  python -c "
+import json; d=json.loads(open('gpurun_out/${T}_b$rep.json').read().strip().splitlines()[-1])
+sb=d['scaling_baseline']
+print('rep $rep: %.3f G cand/s  step %.1f us  kernel %.1f us  pack %.1f us  with-pack step %.1f us (%s)' % (d['value']/1e9, d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, d['exchange']['pack_us'], sb['step_ms_with_pack']*1e3, sb['layout']))"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python bench.py $B > gpurun_out/${T}_prof.log 2>&1 || { tail -5 gpurun_out/${T}_prof.log; exit 1; }
+f=$(find gpurun_out/prof_$T -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/${T}_kernel_stats.csv
+f=$(find gpurun_out/prof_$T -name '*kernel_trace.csv' | head -1); cp "$f" gpurun_out/${T}_kernel_trace.csv; rm -rf gpurun_out/prof_$T
+python -c "
+import csv
+for r in csv.DictReader(open('gpurun_out/${T}_kernel_stats.csv')):
+    print('%-60s %6s %9.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs']) / 1e3))" | head -14
+[ -n "$NO_PROBES" ] && exit 0
+FROM_C=1 TAG=${T}p bash tools/gpu_r5b.sh
