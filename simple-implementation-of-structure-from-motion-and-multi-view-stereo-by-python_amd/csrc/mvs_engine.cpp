@@ -328,6 +328,7 @@ struct mvs_ctx {
     int scorer_wgs = 0;   // env MVS_SCORER_WGS: k_score_tab's grid (0 = every CU, twice)
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
     DevBuf<double> mom_w[MVS_MAX_WID + 1];     // 48 < V <= 64
+    DevBuf<float> mom_wf[MVS_MAX_WID + 1];     // with mom_w: (float)w
     DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V <= 48 or V > 64 (moments_dtab)
     bool mom_ok[MVS_MAX_WID + 1] = {};
     int moments_vp() const { return V > MVS_GROUP_VIEWS ? 64 * ((V + 63) / 64) : 16 * ((V + 15) / 16); }
@@ -335,6 +336,7 @@ struct mvs_ctx {
         MomentsDev m{};
         m.sb = mom_sb[wid].p;
         m.w = mom_w[wid].p;
+        m.wf = mom_wf[wid].p;
         m.d = mom_d[wid].p;
         m.VP = moments_vp();
         m.wid = wid;
@@ -345,9 +347,9 @@ struct mvs_ctx {
     // apply (disabled, or more than 2^31 elements).  One row of 16 pixels
     // past the end: k_score_tab stages a tile's rows whole (16 pixels x VP),
     // also where the last tile column runs past W
-    // Memory: (H W + 16) VP elements per wid, 10 B each at V <= 64 (S_b int16
-    // + w binary64) or 6 B at V > 64 (S_b + D int32): 147 MB per wid at
-    // dinoRing, 3.2 GB at 256 x 1920 x 1080.  A scene past tab_limit elements (2^31;
+    // Memory: (H W + 16) VP elements per wid, 14 B each at V <= 64 (S_b int16
+    // + w binary64 + w binary32) or 6 B at V > 64 (S_b + D int32): 206 MB per
+    // wid at dinoRing, 3.2 GB at 256 x 1920 x 1080.  A scene past tab_limit elements (2^31;
     // env MVS_TAB_LIMIT lowers it, for tests) or whose tables cannot be
     // allocated is scored with the in-kernel moments instead (same results).
     int64_t tab_limit = (int64_t)1 << 31;
@@ -359,19 +361,25 @@ struct mvs_ctx {
             try {
                 mom_sb[wid].alloc((size_t)elems);
                 if (moments_dtab(V)) mom_d[wid].alloc((size_t)elems);
-                else mom_w[wid].alloc((size_t)elems);
+                else {
+                    mom_w[wid].alloc((size_t)elems);
+                    mom_wf[wid].alloc((size_t)elems);
+                }
             } catch (const Fail&) {
                 mom_sb[wid].release();
                 mom_d[wid].release();
                 mom_w[wid].release();
+                mom_wf[wid].release();
                 (void)hipGetLastError();   // the failed hipMalloc's error is not this call's
                 return false;
             }
             HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
             if (moments_dtab(V))
                 HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
-            else
+            else {
                 HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
+                HIPCHK(hipMemsetAsync(mom_wf[wid].p, 0, (size_t)elems * sizeof(float), s));
+            }
             const MomentsDev m = moments(wid);
             if (mvs_launch_moments(&sc, &m, s) != 0) throw Fail{MVS_E_HIP, "moments launch failed"};
             mom_ok[wid] = true;

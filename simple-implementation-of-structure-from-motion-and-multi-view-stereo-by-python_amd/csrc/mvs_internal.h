@@ -141,6 +141,8 @@ struct TiledArgs {
 struct MomentsDev {
     int16_t* sb;
     double* w;      // 48 < V <= 64
+    float* wf;      // beside w: (float)w, the binary32 weight of k_score_tab's decision (its
+                    // binary64 w is then read only for the views that pass)
     int32_t* d;     // moments_dtab(V): V <= 48 or V > 64
     int VP;
     int wid;

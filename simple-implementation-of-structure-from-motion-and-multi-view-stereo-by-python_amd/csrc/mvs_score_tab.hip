@@ -18,6 +18,10 @@
 #include "mvs_device.h"
 #include "mvs_mma.h"
 
+// k_score_tab's SPLIT gather leaves the binary64 weight of a failing lane
+// unset on purpose (its sum term is masked off)
+#pragma clang diagnostic ignored "-Wsometimes-uninitialized"
+
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -108,11 +112,15 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
                     double w = __builtin_amdgcn_rsq(D);
                     w = w * (1.5 - 0.5 * D * w * w);
                     mt.w[o] = w;
+                    mt.wf[o] = (float)w;
                 }
             } else {
                 mt.sb[o] = 0;
                 if constexpr (DTAB) mt.d[o] = -1;
-                else mt.w[o] = __builtin_nan("");
+                else {
+                    mt.w[o] = __builtin_nan("");
+                    mt.wf[o] = __builtin_nanf("");
+                }
             }
         }
     }
@@ -164,6 +172,13 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #endif
 #ifndef MVS_TAB_PIXSORT
 #define MVS_TAB_PIXSORT 0   // A/B switch: sort a wave's candidates by pixel, not by row pair
+#endif
+// MVS_TAB_SPLIT (A/B switch): the decision's weight is gathered as binary32
+// (wf table, 4 B per (candidate, view) instead of 8), and the binary64 w of
+// the sum only for the (candidate, view) pairs that pass (4.5 % of them on
+// the bench's sweep), one candidate step after the decision
+#ifndef MVS_TAB_SPLIT
+#define MVS_TAB_SPLIT 1
 #endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
@@ -246,6 +261,8 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     int32_t* head = t.head;
     const int16_t* __restrict__ tsb = mt.sb;
     const double* __restrict__ tw = mt.w;
+    const float* __restrict__ twf = mt.wf;
+    constexpr bool SPLIT = FAST && !LT && MVS_TAB_SPLIT;
 
     auto region_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_reg1 : s_reg0; };
     auto cand_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_cand1 : s_cand0; };
@@ -463,8 +480,15 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 __builtin_amdgcn_wave_barrier();
                 // the epilogue's table values, one candidate step ahead: lane
                 // (kh, m) needs candidate 4 kh + i's S_b and w_b of views 16 nb + m
+                double sacc[NH][4];
                 int sbv[2][NH][NBLK];
                 double wv[2][NH][NBLK];
+                float wfv[2][NH][NBLK];
+                // SPLIT: a step's passing lanes -- num, the binary64 w being
+                // gathered for them, the pass mask -- summed one step later
+                int numB[2][NH][NBLK];
+                double wB[2][NH][NBLK];
+                uint64_t PB[2][NH][NBLK];
                 auto fetch = [&](auto ic) {
                     constexpr int i = decltype(ic)::value;
 #pragma unroll
@@ -475,11 +499,26 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                             if constexpr (LT) {
                                 sbv[i & 1][h][nb] = ls_sb[tix + 16 * nb];
                                 wv[i & 1][h][nb] = w_of(ls_d[tix + 16 * nb]);
+                            } else if constexpr (SPLIT) {
+                                sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
+                                wfv[i & 1][h][nb] = twf[tix + 16 * nb];
                             } else {
                                 sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
                                 wv[i & 1][h][nb] = tw[tix + 16 * nb];
                             }
                         }
+                    }
+                };
+                // SPLIT: step ip's deferred sum (its w gathers were issued a step ago)
+                auto consume = [&](auto ic) {
+                    constexpr int ip = decltype(ic)::value;
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        double sa = 0.0;
+#pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb)
+                            sa = fma_f64_lanes(sa, numB[ip & 1][h][nb], wB[ip & 1][h][nb], PB[ip & 1][h][nb]);
+                        sacc[h][ip] = sa;
                     }
                 };
                 TSTAMP(tk0);
@@ -595,7 +634,6 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 uint32_t pmv[NH], gdv[NH];
 #pragma unroll
                 for (int h = 0; h < NH; ++h) pmv[h] = gdv[h] = 0u;
-                double sacc[NH][4];
                 static_for<4>([&](auto Ic) {
                     constexpr int i = Ic;
                     if constexpr (i < 3) fetch(std::integral_constant<int, i + 1>{});
@@ -612,9 +650,19 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                             constexpr int nb = Nc;
                             const int vl = 16 * nb + m;
                             const int num = __mul24(c.Sa, sbv[i & 1][h][nb]) + __mul24(NPX, C[h][nb][i]);
-                            const double w = wv[i & 1][h][nb];
                             uint64_t P;
-                            if constexpr (FAST) {
+                            if constexpr (SPLIT) {
+                                // the same binary32 decision ((float)w is the wf entry)
+                                const float x = fmaf((float)num, wfv[i & 1][h][nb], -c.T);
+                                P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
+                                ax[nb] = x;
+                                numB[i & 1][h][nb] = num;
+                                PB[i & 1][h][nb] = P;
+                                double wb;   // lanes that do not pass never read it
+                                if (x > 0.0f) wb = tw[c.tix + m + 16 * nb];   // passing lanes only
+                                wB[i & 1][h][nb] = wb;
+                            } else if constexpr (FAST) {
+                                const double w = wv[i & 1][h][nb];
                                 // ncc > thr <=> num w_b > T; a constant window (w_b nan)
                                 // never passes.  The candidate's own view R passes (its ncc
                                 // is n/(n-1) > thr): its mask bit and its term of the sum
@@ -624,6 +672,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                                 ax[nb] = x;
                                 sa = fma_f64_lanes(sa, num, w, P);
                             } else {
+                                const double w = wv[i & 1][h][nb];
                                 const double ncc = (double)num * w * ca;
                                 const bool pass = vl != c.R && ncc > a.thr;
                                 P = __ballot(pass);
@@ -641,9 +690,12 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         }
                         gdv[h] = writelane<2 * i>(gdv[h], (uint32_t)g);
                         gdv[h] = writelane<2 * i + 1>(gdv[h], (uint32_t)(g >> 32));
-                        sacc[h][i] = sa;
+                        if constexpr (!SPLIT) sacc[h][i] = sa;
                     }
+                    // the previous step's sum: its gathers had this step's decisions to land
+                    if constexpr (SPLIT && i > 0) consume(std::integral_constant<int, i - 1>{});
                 });
+                if constexpr (SPLIT) consume(std::integral_constant<int, 3>{});
                 // owner lane c = 4 j + i (row 0) of each block's candidate c: its mask
                 // bits, guard bits and sum from the lanes that hold them
                 const int jj = m >> 2, ii = m & 3;

@@ -10,12 +10,16 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --time
 rc=$?; tail -2 gpurun_out/${T}_pytest.log; grep "pack_accepted (" gpurun_out/${T}_pytest.log
 if [ $rc -ne 0 ]; then grep -B5 -A40 "FAILED\|Error" gpurun_out/${T}_pytest.log | head -80; [ $rc -ne 1 ] && exit $rc; fi
 B="--no-stage --no-ring --secondary-wid 0 --steps 100 --no-cpu-baseline --no-overlap ${BENCH_ARGS}"
+L0=$PWD/simple-implementation-of-structure-from-motion-and-multi-view-stereo-by-python_amd/libmvs_amd.so
 for rep in 1 2; do
-  timeout -k 10 300 python bench.py $B > gpurun_out/${T}_b$rep.json 2>gpurun_out/${T}_b.err || { tail -5 gpurun_out/${T}_b.err; exit 1; }
-  python -c "
-import json; d=json.loads(open('gpurun_out/${T}_b$rep.json').read().strip().splitlines()[-1])
+  for v in main ${VARIANTS}; do
+    L=$L0; [ $v != main ] && L=${L0%.so}_$v.so
+    MVS_LIB=$L timeout -k 10 300 python bench.py $B > gpurun_out/${T}_b_$v$rep.json 2>gpurun_out/${T}_b.err || { tail -5 gpurun_out/${T}_b.err; exit 1; }
+    python -c "
+import json; d=json.loads(open('gpurun_out/${T}_b_$v$rep.json').read().strip().splitlines()[-1])
 sb=d['scaling_baseline']
-print('rep $rep: %.3f G cand/s  step %.1f us  kernel %.1f us  pack %.1f us  with-pack step %.1f us (%s)' % (d['value']/1e9, d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, d['exchange']['pack_us'], sb['step_ms_with_pack']*1e3, sb['layout']))"
+print('$v rep $rep: %.3f G cand/s  step %.1f us  kernel %.1f us  pack %.1f us  with-pack step %.1f us (%s)' % (d['value']/1e9, d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, d['exchange']['pack_us'], sb['step_ms_with_pack']*1e3, sb['layout']))" | tee -a gpurun_out/${T}_ab.log
+  done
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python bench.py $B > gpurun_out/${T}_prof.log 2>&1 || { tail -5 gpurun_out/${T}_prof.log; exit 1; }
 f=$(find gpurun_out/prof_$T -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/${T}_kernel_stats.csv
