@@ -212,18 +212,20 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
                     "all-gather runs on its own stream behind the next sweep (parallel.PointsExchange)"}
 
 
-def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups=32):
-    """The N = 8 exchange's footprint beside scoring, on one GPU:
-    each step scores the sweep and packs its accepted rows (40 B) on the
-    scoring stream; a second stream waits for the pack and runs a copy kernel
-    of `workgroups` workgroups (RCCL's all-gather is a kernel on a few CUs)
-    moving the bytes one rank receives at N = 8, overlapping the next step.
-    Reported: the step alone, the step with the proxy, and the proxy alone."""
+def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups=32, comm=None):
+    """The N = 8 exchange's footprint beside scoring, on one GPU.
+    Each step scores the sweep on `stream`; the exchange's stream `comm` waits
+    for it, packs the accepted rows (40 B) from the step's record buffer (two
+    alternate) and runs a copy kernel of `workgroups` workgroups moving the
+    bytes one rank receives at N = 8 (RCCL's all-gather is a kernel on a few
+    CUs streaming bytes), overlapping the next step.  With the multi-GPU
+    layout, `stream` is CU-masked and `comm` holds the CUs it leaves out.
+    Reported: the step with its pack alone, with the proxy copy too, and the
+    copy alone on `comm`."""
     import torch
     pkg = importlib.import_module(PKG_NAME)
     par = importlib.import_module(PKG_NAME + ".parallel")
     dev = sw["c"].device
-    pc, pm = pack_src(sw)
     words = (V + 63) // 64
     width = par.points_width(words)
     cap = accepted + accepted // 16 + 256
@@ -231,18 +233,26 @@ def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups
     src = torch.zeros(recv // 8, dtype=torch.int64, device=dev)
     dst = torch.empty_like(src)
     out = torch.empty((cap + 1, width), dtype=torch.int64, device=dev)
-    comm = torch.cuda.Stream(dev)
+    comm = comm if comm is not None else torch.cuda.Stream(dev)
+    recs = sw.get("recs") or [sw["rec"], sw["rec"]]
+    read = [None, None]
 
     def run(k, with_proxy):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(k):
-            score(ctx, sw, wid, thr, stream)
-            ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
+        for st in range(k):
+            b = st & 1
+            if read[b] is not None and not read[b].query():
+                stream.wait_event(read[b])
+            score(ctx, sw, wid, thr, stream, recs[b] if sw["rec"] is not None else None)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            comm.wait_event(ev)
+            pc, pm = pack_src(sw, recs[b] if sw["rec"] is not None else None)
+            ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=comm.cuda_stream, c=sw["c"])
+            read[b] = torch.cuda.Event()
+            read[b].record(comm)
             if with_proxy:
-                ev = torch.cuda.Event()
-                ev.record(stream)
-                comm.wait_event(ev)
                 pkg._lib.proxy_copy(dst, src, recv, workgroups, comm.cuda_stream)
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / k
@@ -256,8 +266,8 @@ def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups
         pkg._lib.proxy_copy(dst, src, recv, workgroups, comm.cuda_stream)
     e1.record(comm)
     e1.synchronize()
-    return {"proxy": f"copy kernel of {workgroups} workgroups moving the N = 8 per-rank receive "
-                     f"({recv / 1e6:.1f} MB of 40-B rows) on a second stream after each step's pack",
+    return {"proxy": f"pack + copy kernel of {workgroups} workgroups moving the N = 8 per-rank receive "
+                     f"({recv / 1e6:.1f} MB of 40-B rows) on the exchange's stream after each step's scoring",
             "step_us_score_pack": alone * 1e6, "step_us_with_proxy": both * 1e6,
             "proxy_alone_us": e0.elapsed_time(e1) / 10 * 1e3, "received_bytes": recv, "workgroups": workgroups}
 
@@ -414,7 +424,10 @@ def main():
                 # stream packs sweep k's from the other
                 b = ex.posted & 1
                 rec = sw["recs"][b]
-                if ex.consumed(b) is not None:
+                # a cross-stream wait costs the scoring stream ~18 us of dead
+                # time (profiles/r05/r5c_masked_pack_on_comm_timeline.txt):
+                # enqueue it only while the pack two sweeps back is still running
+                if ex.consumed(b) is not None and not ex.consumed(b).query():
                     st.wait_event(ex.consumed(b))
             if evs is not None:
                 evs[0].record(st)
@@ -468,9 +481,10 @@ def main():
     # (all CUs but --comm-cus), the scorer's grid at two workgroups per kept
     # CU, and the pack + all-gather on the exchange's stream, where they find
     # the free CUs instead of queueing behind the persistent scorer
-    mstream, kept = stream, None
+    mstream, kept, cstream = stream, None, None
     if a.comm_cus > 0 and (world > 1 or rank == 0):
         mstream, kept = par.cu_masked_stream(dev, a.comm_cus)
+        cstream, _ = par.cu_masked_stream(dev, a.comm_cus, complement=True)
 
     def masked(on):
         ctx.set_scorer_grid(2 * kept if on and kept else 0)
@@ -484,7 +498,8 @@ def main():
         kk = torch.tensor([int((host_outputs(sw)[1] >= vlb).sum())], dtype=torch.int64, device=dev)
         dist.all_reduce(kk, op=dist.ReduceOp.MAX)
         cap = int(kk.item()) + int(kk.item()) // 16 + 256
-        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap, dev, pack_on_comm=pack_on_comm)
+        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap, dev, pack_on_comm=pack_on_comm,
+                                        comm_stream=cstream if pack_on_comm else None)
         masked(True)
     total_n = a.n if a.strong else a.n * world
     dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream if world > 1 else stream)
@@ -503,7 +518,8 @@ def main():
         # score + the 40-B point pack (PointsExchange at world 1), so that a
         # 1 -> N comparison can also be made on the same device work
         cap1 = accepted + accepted // 16 + 256
-        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap1, dev, pack_on_comm=pack_on_comm)
+        sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap1, dev, pack_on_comm=pack_on_comm,
+                                        comm_stream=cstream if pack_on_comm else None)
         masked(True)
         pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream)
         masked(False)
@@ -514,7 +530,8 @@ def main():
                         "step_ms_score_only": dt / a.steps * 1e3,
                         "layout": (f"scoring on {kept} of {kept + a.comm_cus} CUs (CU-masked stream), " if kept else
                                    "scoring on every CU, ") +
-                                  ("pack on the exchange's stream" if pack_on_comm else "pack on the scoring stream"),
+                                  ((f"pack on the exchange's stream ({a.comm_cus} CUs)" if kept else
+                                    "pack on the exchange's stream") if pack_on_comm else "pack on the scoring stream"),
                         "note": "`value` at N = 1 is the scoring step alone (no exchange exists on one GPU); "
                                 "at N > 1 a step adds the 40-B point pack and the all-gather (overlapped "
                                 "with the next sweep). value_with_pack is the N = 1 step with the pack"}
@@ -561,18 +578,20 @@ def main():
     }
     out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms, kernel_name)
     if solo and not a.no_overlap:
-        ov = overlap_proxy(ctx, sw, V, vlb, accepted, stream, a.thr, a.wid, max(a.steps // 2, 10))
-        # the same with the scorer held to 448 workgroups (224 CUs), leaving
-        # 32 CUs to the collective's kernel
-        os.environ["MVS_SCORER_WGS"] = "448"
+        # the multi-GPU layout: scoring on the CU-masked stream, the pack and
+        # the proxy of RCCL's all-gather on the CUs it leaves out
+        masked(True)
         try:
-            ctx2 = pkg.MvsContext(rgb, K, R, t, device=local)
+            ov = overlap_proxy(ctx, sw, V, vlb, accepted, mstream, a.thr, a.wid, max(a.steps // 2, 10),
+                               comm=cstream)
         finally:
-            del os.environ["MVS_SCORER_WGS"]
-        ov["scorer_448_workgroups"] = {k: v for k, v in overlap_proxy(
-            ctx2, sw, V, vlb, accepted, stream, a.thr, a.wid, max(a.steps // 2, 10)).items()
-            if "_us" in k}
-        ctx2.close()
+            masked(False)
+        ov["layout"] = (f"scoring on {kept} CUs (CU-masked stream), pack + copy on the other {a.comm_cus}"
+                        if kept else "scoring and exchange on every CU")
+        # for comparison: one unmasked stream each (the copy then competes
+        # for the CUs the persistent scorer holds)
+        ov["unmasked"] = {k: v for k, v in overlap_proxy(
+            ctx, sw, V, vlb, accepted, stream, a.thr, a.wid, max(a.steps // 2, 10)).items() if "_us" in k}
         out["exchange"]["overlap_proxy"] = ov
 
     if solo:
@@ -671,6 +690,10 @@ def main():
 
     if rank == 0:
         print(json.dumps(out))
+    sw.pop("exch", None)
+    for s_ in (mstream, cstream):
+        if s_ is not None and s_ is not stream:
+            par.destroy_stream(s_)
     if world > 1:
         dist.destroy_process_group()
     ctx.close()

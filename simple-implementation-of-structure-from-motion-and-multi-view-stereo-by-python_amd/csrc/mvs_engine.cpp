@@ -347,9 +347,9 @@ struct mvs_ctx {
     // apply (disabled, or more than 2^31 elements).  One row of 16 pixels
     // past the end: k_score_tab stages a tile's rows whole (16 pixels x VP),
     // also where the last tile column runs past W
-    // Memory: (H W + 16) VP elements per wid, 14 B each at V <= 64 (S_b int16
-    // + w binary64 + w binary32) or 6 B at V > 64 (S_b + D int32): 206 MB per
-    // wid at dinoRing, 3.2 GB at 256 x 1920 x 1080.  A scene past tab_limit elements (2^31;
+    // Memory: (H W + 16) VP elements per wid, 10 B each at V <= 64 (S_b int16
+    // + w binary64; + 4 B of binary32 w with MVS_TAB_SPLIT) or 6 B at V > 64
+    // (S_b + D int32): 147 MB per wid at dinoRing, 3.2 GB at 256 x 1920 x 1080.  A scene past tab_limit elements (2^31;
     // env MVS_TAB_LIMIT lowers it, for tests) or whose tables cannot be
     // allocated is scored with the in-kernel moments instead (same results).
     int64_t tab_limit = (int64_t)1 << 31;
@@ -363,7 +363,7 @@ struct mvs_ctx {
                 if (moments_dtab(V)) mom_d[wid].alloc((size_t)elems);
                 else {
                     mom_w[wid].alloc((size_t)elems);
-                    mom_wf[wid].alloc((size_t)elems);
+                    if (MVS_TAB_SPLIT) mom_wf[wid].alloc((size_t)elems);
                 }
             } catch (const Fail&) {
                 mom_sb[wid].release();
@@ -378,7 +378,7 @@ struct mvs_ctx {
                 HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
             else {
                 HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
-                HIPCHK(hipMemsetAsync(mom_wf[wid].p, 0, (size_t)elems * sizeof(float), s));
+                if (mom_wf[wid].p) HIPCHK(hipMemsetAsync(mom_wf[wid].p, 0, (size_t)elems * sizeof(float), s));
             }
             const MomentsDev m = moments(wid);
             if (mvs_launch_moments(&sc, &m, s) != 0) throw Fail{MVS_E_HIP, "moments launch failed"};

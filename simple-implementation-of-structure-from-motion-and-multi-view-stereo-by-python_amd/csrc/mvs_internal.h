@@ -93,6 +93,14 @@ inline int64_t tc_words(int ntiles) { return (int64_t)ntiles * kTcStride + (3 + 
 #define MVS_TAB_LT_VIEWS 0
 #endif
 inline bool moments_dtab(int V) { return V <= MVS_TAB_LT_VIEWS || V > 64; }
+// k_score_tab A/B switch: the decision's weight gathered as binary32 from a
+// wf table (4 B per (candidate, view) instead of 8) and the binary64 w of the
+// sum only for the passing pairs (4.5 % of them on the bench's sweep), one
+// candidate step after the decision.  Measured slower (120 vs 106 us per
+// 2^20, profiles/r05/r5c_ab_split_implicit.log): off, and no wf table then
+#ifndef MVS_TAB_SPLIT
+#define MVS_TAB_SPLIT 0
+#endif
 
 struct TiledArgs {
     int ntx, nty, ntiles;

@@ -2047,18 +2047,15 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // Chunks of kAccPer x kAccThreads = 2,048 candidates, thread t of a chunk
 // holding candidates chunk + t + kAccThreads j (j < kAccPer): the reads stay
 // coalesced, a 2^20 slice has 512 chunks (two workgroups on every CU), and
-// the look-back reads 512-chunk windows (one window for such a slice).  All
-// of a chunk's loads are issued at once -- first mask words, counts (records:
-// the count IS the popcount) and every candidate's point (a 24-B stride over
-// the slice: nearly every line holds an accepted point anyway) -- and stay in
-// flight across the scan and look-back (LDS-only barriers).  The accepted
-// rows are assembled in LDS in index order and leave as one contiguous run of
-// 16-B stores (rows of 40 B: the run starts 8-B aligned).
+// the look-back reads 512-chunk windows (one window for such a slice).  Each candidate's first
+// mask word is loaded with its count (records: the count IS its popcount), the
+// accepted candidates' points as soon as the counts are in; they stay in
+// flight across the chunk's scan and look-back (LDS-only barriers), so that
+// the rows go out as soon as the prefix is in.
 constexpr int kAccThreads = 256, kAccPer = 8, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
 constexpr int kAccE = kAccPer * kAccWaves;          // (j, wave) counts of a chunk
 constexpr int kAccEpl = (kAccE + 63) / 64;          // of them per lane of wave 0's scan
 constexpr int kAccLB = 8;                            // status words per lane of the look-back window
-constexpr int kAccStage = 40 * 1024;                 // LDS bytes of a chunk's staged rows
 // 16-B accesses at 8-B alignment (global_load/store_dwordx4 allow it)
 typedef double acc_d2v __attribute__((ext_vector_type(2)));
 typedef acc_d2v acc_d2 __attribute__((aligned(8)));
@@ -2071,20 +2068,18 @@ static_assert(kAccE <= 128, "wave 0 scans at most two (j, wave) counts per lane"
 // count, found by a decoupled look-back over per-chunk status words
 // (epoch << 34 | flag << 32 | value; flag 1 = the chunk's own count, 2 = the
 // inclusive count through it; a word of another epoch is not yet published).
-// Chunks are handed out by a ticket (err[1]) in the order workgroups ask, so
-// a chunk's predecessors all belong to workgroups that are running; a kernel
-// sharing the CUs (RCCL's, the next sweep's scorer) can still slow them, so
-// every wait is bounded in time (kAccWaitTicks of the 100 MHz real-time
-// clock): on expiry the chunk takes the slow path that depends on no other
-// workgroup -- the whole workgroup counts the accepted candidates before it
-// from the inputs -- and publishes that exact prefix (so no result is ever
-// wrong); err[0] counts these fall-backs (mvs_pack_fallbacks).  The words are
-// relaxed agent-scope atomics: a word carries all a reader needs, and a
-// release or acquire would write back or invalidate this XCD's L2 at every
-// step.  The workgroup that draws the last ticket returns the ticket to 0.
-// debug (tests only): > 0 = a spin limit in look-back rounds; < 0 = chunk
-// -debug falls back at once.
-constexpr int kAccGrid = 2048;
+// One workgroup per chunk, dispatched in index order, so a chunk waits only
+// for earlier chunks' workgroups, which have started (however many chunks
+// there are); but a kernel sharing the CUs (RCCL's, the next sweep's scorer)
+// can delay them, so every wait is bounded in time (kAccWaitTicks of the
+// 100 MHz real-time clock, the wave sleeping between polls):
+// on expiry the chunk takes the slow path that depends on no other workgroup
+// -- the whole workgroup counts the accepted candidates before it from the
+// inputs -- and publishes that exact prefix (so no result is ever wrong);
+// *err counts these fall-backs (mvs_pack_fallbacks).  The words are relaxed
+// agent-scope atomics: a word carries all a reader needs, and a release or
+// acquire would write back or invalidate this XCD's L2 at every step.
+// debug (tests only): > 0 = a limit in polls; < 0 = chunk -debug falls back at once.
 constexpr uint64_t kAccWaitTicks = 20000;            // 200 us
 
 DEV int acc_count(const int32_t* __restrict__ count, const uint64_t* __restrict__ mask, int64_t ms, int words,
@@ -2101,47 +2096,28 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                                                           uint64_t epoch, int32_t* __restrict__ err, int64_t debug,
                                                           int64_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
-    __shared__ __attribute__((aligned(16))) int64_t s_rows[kAccStage / 8];
     __shared__ int64_t s_base;
-    __shared__ int s_slow, s_b;
+    __shared__ int s_slow;
     __shared__ int64_t s_total;
     __shared__ int64_t s_part[kAccWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int width = 1 + words + (cpt ? 3 : 0);
-    const int stage_rows = kAccStage / (8 * width);
     // count == null: the scorer's records [mask words, avg], |V| = popcount
     const int64_t ms = count ? words : words + 1;
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     const int64_t nch = nchunk > 0 ? nchunk : 1;      // an empty slice still has chunk 0, which writes the header
     const uint64_t E = epoch << 34;
-    int32_t* ticket = err + 1;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // tickets nch .. nch + grid - 1 end the workgroups; the last one resets
-            if (tk == nch + (int64_t)gridDim.x - 1) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_b = tk;
-        }
-        __syncthreads();
-        const int64_t b = s_b;
-        if (b >= nch) break;
-        // every load of the chunk in flight at once
+    {
+        const int64_t b = blockIdx.x;
+        // every load of the chunk in flight at once: the first mask words and
+        // the counts (records: popcounts of the words)
         uint64_t m[kAccPer], w0[kAccPer];
         int c[kAccPer];
-        double px[kAccPer], py[kAccPer], pz[kAccPer];
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
             w0[j] = i < n ? mask[i * ms] : 0ull;
             c[j] = i < n && count ? count[i] : 0;
-            px[j] = py[j] = pz[j] = 0.0;
-            if (cpt && i < n) {
-                // x, y as one 16-B load (8-B aligned), z beside it
-                const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
-                px[j] = xy.x;
-                py[j] = xy.y;
-                pz[j] = cpt[3 * i + 2];
-            }
         }
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
@@ -2151,10 +2127,20 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 for (int q = 1; q < words; ++q) c[j] += __popcll(mask[i * ms + q]);
             }
         }
+        double px[kAccPer], py[kAccPer], pz[kAccPer];
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            m[j] = __ballot(i < n && c[j] >= vlb);
+            const bool acc = i < n && c[j] >= vlb;
+            m[j] = __ballot(acc);
+            px[j] = py[j] = pz[j] = 0.0;
+            if (cpt && acc) {
+                // x, y as one 16-B load (8-B aligned), z beside it
+                const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
+                px[j] = xy.x;
+                py[j] = xy.y;
+                pz[j] = cpt[3 * i + 2];
+            }
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
         }
         lds_barrier();   // the points stay in flight
@@ -2190,7 +2176,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                                    __HIP_MEMORY_SCOPE_AGENT);
             uint64_t excl = 0;
             int64_t top = b - 1;          // the window's highest chunk
-            uint32_t rounds = 0;
+            uint32_t polls = 0;
             uint64_t t_start = 0;
             bool slow = debug < 0 && b == -debug;
             constexpr int WIN = 64 * kAccLB;
@@ -2216,8 +2202,8 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 if (d_unpub < d_incl) {
                     // a chunk in the window has not published yet
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                    if (rounds++ == 0) t_start = now;
-                    if (debug > 0 ? rounds > (uint32_t)debug : now - t_start > kAccWaitTicks) slow = true;
+                    if (polls++ == 0) t_start = now;
+                    if (debug > 0 ? polls > (uint32_t)debug : now - t_start > kAccWaitTicks) slow = true;
                     __builtin_amdgcn_s_sleep(2);
                     continue;
                 }
@@ -2277,44 +2263,33 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             __syncthreads();
         }
         const int64_t base = s_base;
-        // rows [base, base + nrows) of the chunk fit the capacity; the first
-        // stage_rows of them are assembled in LDS, the rest stored directly
-        const int64_t nrows = min((int64_t)s_total, max(cap - base, (int64_t)0));
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             if ((m[j] >> lane) & 1ull) {
                 const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-                const int loc = s_cnt[j * kAccWaves + wave] +
-                                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
-                if (loc >= nrows) continue;
-                int64_t* o = loc < stage_rows ? s_rows + (int64_t)loc * width : out + (1 + base + loc) * width;
-                o[0] = offset + i;
-                o[1] = (int64_t)w0[j];
-                for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
-                if (cpt) {
-                    // the accepted 3D point itself (binary64 bits)
-                    o[1 + words] = __double_as_longlong(px[j]);
-                    o[2 + words] = __double_as_longlong(py[j]);
-                    o[3 + words] = __double_as_longlong(pz[j]);
+                const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
+                                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
+                if (pos < cap && words == 1 && cpt) {
+                    // the 40-B row as 16 + 16 + 8 B (8-B aligned stores)
+                    int64_t* o = out + (1 + pos) * width;
+                    *(acc_l2*)o = acc_l2{offset + i, (int64_t)w0[j]};
+                    *(acc_l2*)(o + 2) = acc_l2{__double_as_longlong(px[j]), __double_as_longlong(py[j])};
+                    o[4] = __double_as_longlong(pz[j]);
+                } else if (pos < cap) {
+                    int64_t* o = out + (1 + pos) * width;
+                    o[0] = offset + i;
+                    o[1] = (int64_t)w0[j];
+                    for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
+                    if (cpt) {
+                        // the accepted 3D point itself (binary64 bits)
+                        o[1 + words] = __double_as_longlong(px[j]);
+                        o[2 + words] = __double_as_longlong(py[j]);
+                        o[3 + words] = __double_as_longlong(pz[j]);
+                    }
                 }
             }
         }
-        lds_barrier();
-        // the staged rows: one contiguous run of nq 8-B words from word
-        // (1 + base) width of out, written as 16-B stores (an 8-B head where
-        // the run starts at 8 mod 16, an 8-B tail where it ends there)
-        {
-            const int64_t nq = min(nrows, (int64_t)stage_rows) * width;
-            int64_t* dst = out + (1 + base) * width;
-            const int head = ((uintptr_t)dst & 15) ? 1 : 0;
-            if (threadIdx.x == 0 && head && nq > 0) dst[0] = s_rows[0];
-            const int64_t npair = (nq - head) >> 1;
-            for (int64_t p = threadIdx.x; p < npair; p += kAccThreads)
-                *(acc_l2*)(dst + head + 2 * p) = acc_l2{s_rows[head + 2 * p], s_rows[head + 2 * p + 1]};
-            if (threadIdx.x == 0 && nq > head && ((nq - head) & 1)) dst[nq - 1] = s_rows[nq - 1];
-        }
-        __syncthreads();   // s_cnt, s_rows and s_b are rewritten by the next chunk
     }
 }
 
@@ -2670,7 +2645,8 @@ extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t
                                         const double* c, int words, int vlb, int64_t cap, uint64_t* status,
                                         uint64_t epoch, int32_t* err, int64_t debug, int64_t* out, hipStream_t s) {
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nchunk, kAccGrid));
+    if (nchunk >= ((int64_t)1 << 31)) return -3;
+    const int grid = (int)std::max<int64_t>(1, nchunk);   // one workgroup per chunk
     // n == 0 still writes the header (chunk 0 of an empty slice)
     hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, c, words, vlb, cap,
                        status, epoch, err, debug, out);

@@ -112,14 +112,14 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
                     double w = __builtin_amdgcn_rsq(D);
                     w = w * (1.5 - 0.5 * D * w * w);
                     mt.w[o] = w;
-                    mt.wf[o] = (float)w;
+                    if (mt.wf) mt.wf[o] = (float)w;
                 }
             } else {
                 mt.sb[o] = 0;
                 if constexpr (DTAB) mt.d[o] = -1;
                 else {
                     mt.w[o] = __builtin_nan("");
-                    mt.wf[o] = __builtin_nanf("");
+                    if (mt.wf) mt.wf[o] = __builtin_nanf("");
                 }
             }
         }
@@ -173,13 +173,8 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_PIXSORT
 #define MVS_TAB_PIXSORT 0   // A/B switch: sort a wave's candidates by pixel, not by row pair
 #endif
-// MVS_TAB_SPLIT (A/B switch): the decision's weight is gathered as binary32
-// (wf table, 4 B per (candidate, view) instead of 8), and the binary64 w of
-// the sum only for the (candidate, view) pairs that pass (4.5 % of them on
-// the bench's sweep), one candidate step after the decision
-#ifndef MVS_TAB_SPLIT
-#define MVS_TAB_SPLIT 1
-#endif
+// MVS_TAB_SPLIT (A/B switch, mvs_internal.h): measured slower, 120 vs 106 us
+// per 2^20 (profiles/r05/r5c_ab_split_implicit.log)
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD

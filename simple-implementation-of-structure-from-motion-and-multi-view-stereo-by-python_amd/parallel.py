@@ -25,31 +25,58 @@ import torch
 import torch.distributed as dist
 
 
-def cu_masked_stream(device, free_cus):
+def cu_masked_stream(device, free_cus, complement=False):
     """A stream of `device` whose kernels run on all CUs but `free_cus` of
     them (hipExtStreamCreateWithCUMask; bit k of the mask = CU k as HIP
-    numbers them, the highest free_cus left out), as a torch ExternalStream,
-    and the number of CUs it keeps.  The multi-GPU step scores on such a
-    stream with the scorer's grid at two workgroups per kept CU
-    (MvsContext.set_scorer_grid), so that the exchange's pack and RCCL's
-    all-gather kernels find CUs of their own instead of waiting for the
-    persistent scorer's workgroups (bench.py)."""
+    numbers them, the highest free_cus left out), or with complement=True
+    on those free_cus CUs only; as (torch ExternalStream, CUs in its mask).
+    The multi-GPU step scores on the first kind, with the scorer's grid at
+    two workgroups per CU of the mask (MvsContext.set_scorer_grid), and
+    packs its accepted points on the second (PointsExchange): the exchange
+    then never takes CUs from the next sweep's kernels.
+    Release it with destroy_stream()."""
     import ctypes
     dev = torch.device(device)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    keep = max(ncu - int(free_cus), 1)
+    free = min(max(int(free_cus), 1), ncu - 1)
+    lo, hi = (ncu - free, ncu) if complement else (0, ncu - free)
     words = []
     for w in range((ncu + 31) // 32):
-        lo, hi = 32 * w, min(32 * w + 32, keep)
-        words.append(((1 << (hi - lo)) - 1) if hi > lo else 0)
-    hip = ctypes.CDLL("libamdhip64.so")
+        v = 0
+        for b in range(32):
+            if lo <= 32 * w + b < hi:
+                v |= 1 << b
+        words.append(v)
     arr = (ctypes.c_uint32 * len(words))(*words)
     handle = ctypes.c_void_p()
     with torch.cuda.device(dev):
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), arr)
+        rc = _hip().hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), arr)
     if rc != 0:
         raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    return torch.cuda.ExternalStream(handle.value, device=dev), keep
+    return torch.cuda.ExternalStream(handle.value, device=dev), hi - lo
+
+
+def destroy_stream(stream):
+    """Release a stream of cu_masked_stream (after its work has completed)."""
+    stream.synchronize()
+    _hip().hipStreamDestroy(ctypes_void_p(stream.cuda_stream))
+
+
+def ctypes_void_p(x):
+    import ctypes
+    return ctypes.c_void_p(x)
+
+
+_HIP = None
+
+
+def _hip():
+    """The HIP runtime torch loaded (its libamdhip64)."""
+    global _HIP
+    if _HIP is None:
+        import ctypes
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    return _HIP
 
 
 def shard_range(n, rank, world):
@@ -105,7 +132,7 @@ class PointsExchange:
     ctx = the rank's MvsContext (its pack kernel); on CPU tensors (gloo) the
     torch reference pack is used and the all-gather is synchronous."""
 
-    def __init__(self, ctx, words, cap, device, group=None, points=True, pack_on_comm=False):
+    def __init__(self, ctx, words, cap, device, group=None, points=True, pack_on_comm=False, comm_stream=None):
         self.ctx, self.words, self.cap, self.group = ctx, words, int(cap), group
         self.points = bool(points)
         # pack_on_comm: the pack runs on the communication stream as well (after
@@ -120,8 +147,10 @@ class PointsExchange:
         self.send = [torch.zeros((self.cap + 1, self.width), dtype=torch.int64, device=device) for _ in range(2)]
         self.recv = [torch.zeros((self.world * (self.cap + 1), self.width), dtype=torch.int64, device=device)
                      for _ in range(2)]
-        self.comm = (torch.cuda.Stream(self.device) if cuda and (self.world > 1 or self.pack_on_comm)
-                     else None)
+        # comm_stream: e.g. a cu_masked_stream(complement=True) of the CUs the
+        # scoring stream leaves out
+        self.comm = comm_stream if comm_stream is not None else (
+            torch.cuda.Stream(self.device) if cuda and (self.world > 1 or self.pack_on_comm) else None)
         self.done = [None, None]
         self.posted = 0
 
