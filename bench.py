@@ -214,14 +214,13 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
 
 def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups=32, comm=None):
     """The N = 8 exchange's footprint beside scoring, on one GPU.
-    Each step scores the sweep on `stream`; the exchange's stream `comm` waits
-    for it, packs the accepted rows (40 B) from the step's record buffer (two
-    alternate) and runs a copy kernel of `workgroups` workgroups moving the
-    bytes one rank receives at N = 8 (RCCL's all-gather is a kernel on a few
-    CUs streaming bytes), overlapping the next step.  With the multi-GPU
-    layout, `stream` is CU-masked and `comm` holds the CUs it leaves out.
-    Reported: the step with its pack alone, with the proxy copy too, and the
-    copy alone on `comm`."""
+    Each step scores the sweep and packs its accepted rows (40 B) on
+    `stream`; the stream `comm` waits for the pack and runs a copy kernel of
+    `workgroups` workgroups moving the bytes one rank receives at N = 8
+    (RCCL's all-gather is a kernel on a few CUs streaming bytes), overlapping
+    the next step.  With the multi-GPU layout `stream` is CU-masked and
+    `comm` holds the CUs it leaves out.  Reported: the step (score + pack)
+    alone, with the proxy copy too, and the copy alone on `comm`."""
     import torch
     pkg = importlib.import_module(PKG_NAME)
     par = importlib.import_module(PKG_NAME + ".parallel")
@@ -234,25 +233,17 @@ def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups
     dst = torch.empty_like(src)
     out = torch.empty((cap + 1, width), dtype=torch.int64, device=dev)
     comm = comm if comm is not None else torch.cuda.Stream(dev)
-    recs = sw.get("recs") or [sw["rec"], sw["rec"]]
-    read = [None, None]
-
     def run(k, with_proxy):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for st in range(k):
-            b = st & 1
-            if read[b] is not None and not read[b].query():
-                stream.wait_event(read[b])
-            score(ctx, sw, wid, thr, stream, recs[b] if sw["rec"] is not None else None)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            comm.wait_event(ev)
-            pc, pm = pack_src(sw, recs[b] if sw["rec"] is not None else None)
-            ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=comm.cuda_stream, c=sw["c"])
-            read[b] = torch.cuda.Event()
-            read[b].record(comm)
+            score(ctx, sw, wid, thr, stream)
+            pc, pm = pack_src(sw)
+            ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
             if with_proxy:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                comm.wait_event(ev)
                 pkg._lib.proxy_copy(dst, src, recv, workgroups, comm.cuda_stream)
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / k
@@ -266,8 +257,8 @@ def overlap_proxy(ctx, sw, V, vlb, accepted, stream, thr, wid, steps, workgroups
         pkg._lib.proxy_copy(dst, src, recv, workgroups, comm.cuda_stream)
     e1.record(comm)
     e1.synchronize()
-    return {"proxy": f"pack + copy kernel of {workgroups} workgroups moving the N = 8 per-rank receive "
-                     f"({recv / 1e6:.1f} MB of 40-B rows) on the exchange's stream after each step's scoring",
+    return {"proxy": f"copy kernel of {workgroups} workgroups moving the N = 8 per-rank receive "
+                     f"({recv / 1e6:.1f} MB of 40-B rows) on a second stream after each step's pack",
             "step_us_score_pack": alone * 1e6, "step_us_with_proxy": both * 1e6,
             "proxy_alone_us": e0.elapsed_time(e1) / 10 * 1e3, "received_bytes": recv, "workgroups": workgroups}
 
@@ -332,9 +323,9 @@ def main():
     ap.add_argument("--comm-cus", type=int, default=16,
                     help="N > 1 (and the N = 1 with-pack baseline): CUs left out of the scoring stream's "
                          "CU mask for the exchange's pack and all-gather (0: no mask)")
-    ap.add_argument("--pack-on-scoring-stream", action="store_true",
-                    help="N > 1: pack on the scoring stream (default: on the exchange's stream, overlapping "
-                         "the next sweep)")
+    ap.add_argument("--pack-on-comm", action="store_true",
+                    help="N > 1: pack on the exchange's stream (the CUs the masked scoring stream leaves "
+                         "out), overlapping the next sweep (default: on the scoring stream, after the sweep)")
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
                     help="headline scene (ring256: config 4 as the headline, for profiling)")
     argv = json.loads(os.environ["MVS_BENCH_ARGV"]) if "MVS_BENCH_ARGV" in os.environ else None
@@ -489,7 +480,7 @@ def main():
     def masked(on):
         ctx.set_scorer_grid(2 * kept if on and kept else 0)
 
-    pack_on_comm = not a.pack_on_scoring_stream
+    pack_on_comm = a.pack_on_comm
     if world > 1:
         # exchange capacity: this sweep's accepted count (one untimed score),
         # the maximum over ranks plus a margin (rows of every rank are equal-sized)
@@ -531,7 +522,8 @@ def main():
                         "layout": (f"scoring on {kept} of {kept + a.comm_cus} CUs (CU-masked stream), " if kept else
                                    "scoring on every CU, ") +
                                   ((f"pack on the exchange's stream ({a.comm_cus} CUs)" if kept else
-                                    "pack on the exchange's stream") if pack_on_comm else "pack on the scoring stream"),
+                                    "pack on the exchange's stream") if pack_on_comm else
+                                   "pack on the scoring stream, the gather's CUs left free"),
                         "note": "`value` at N = 1 is the scoring step alone (no exchange exists on one GPU); "
                                 "at N > 1 a step adds the 40-B point pack and the all-gather (overlapped "
                                 "with the next sweep). value_with_pack is the N = 1 step with the pack"}
@@ -586,7 +578,7 @@ def main():
                                comm=cstream)
         finally:
             masked(False)
-        ov["layout"] = (f"scoring on {kept} CUs (CU-masked stream), pack + copy on the other {a.comm_cus}"
+        ov["layout"] = (f"scoring + pack on {kept} CUs (CU-masked stream), copy on the other {a.comm_cus}"
                         if kept else "scoring and exchange on every CU")
         # for comparison: one unmasked stream each (the copy then competes
         # for the CUs the persistent scorer holds)

@@ -2298,18 +2298,19 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
 // kernel (a few CUs streaming bytes) -- to run beside the scoring kernels.
 // Eight pieces per thread in flight, as a collective's copy loop keeps them
 // (one at a time makes the copy latency-bound: 3x slower beside the scorer,
-// profiles/r05/r5a_timeline.txt).
+// profiles/r05/r5a_overlap_probe_timeline_old_proxy.txt).
 __global__ __launch_bounds__(256) void k_proxy_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
     constexpr int U = 8;
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += U * stride) {
+    // one contiguous range per workgroup, U coalesced 4-KiB pieces in flight
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(n, b0 + per);
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += 256 * U) {
         uint4 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (i0 + u * stride < n) v[u] = src[i0 + u * stride];
+        for (int u = 0; u < U; ++u) v[u] = i + 256 * u < b1 ? src[i + 256 * u] : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (i0 + u * stride < n) dst[i0 + u * stride] = v[u];
+            if (i + 256 * u < b1) dst[i + 256 * u] = v[u];
     }
 }
 
