@@ -321,8 +321,11 @@ def main():
     ap.add_argument("--soa", action="store_true",
                     help="score into the three output arrays (mask, count, avg) instead of one record per candidate")
     ap.add_argument("--comm-cus", type=int, default=16,
-                    help="N > 1 (and the N = 1 with-pack baseline): CUs left out of the scoring stream's "
-                         "CU mask for the exchange's pack and all-gather (0: no mask)")
+                    help="N > 1 (and the N = 1 with-pack baseline): CUs left to the all-gather's kernel "
+                         "(0: none)")
+    ap.add_argument("--comm-layout", choices=["mask", "grid"], default="mask",
+                    help="how --comm-cus are kept free: a CU-masked scoring stream (mask) or the "
+                         "persistent scorer's grid at two workgroups per remaining CU (grid)")
     ap.add_argument("--pack-on-comm", action="store_true",
                     help="N > 1: pack on the exchange's stream (the CUs the masked scoring stream leaves "
                          "out), overlapping the next sweep (default: on the scoring stream, after the sweep)")
@@ -474,8 +477,11 @@ def main():
     # the free CUs instead of queueing behind the persistent scorer
     mstream, kept, cstream = stream, None, None
     if a.comm_cus > 0 and (world > 1 or rank == 0):
-        mstream, kept = par.cu_masked_stream(dev, a.comm_cus)
-        cstream, _ = par.cu_masked_stream(dev, a.comm_cus, complement=True)
+        if a.comm_layout == "mask":
+            mstream, kept = par.cu_masked_stream(dev, a.comm_cus)
+            cstream, _ = par.cu_masked_stream(dev, a.comm_cus, complement=True)
+        else:
+            kept = torch.cuda.get_device_properties(dev).multi_processor_count - a.comm_cus
 
     def masked(on):
         ctx.set_scorer_grid(2 * kept if on and kept else 0)
@@ -519,7 +525,9 @@ def main():
             raise RuntimeError(f"N = 1 pack: {packed} rows != {accepted} accepted")
         scaling_base = {"step_ms_with_pack": pdt / a.steps * 1e3, "value_with_pack": n * a.steps / pdt,
                         "step_ms_score_only": dt / a.steps * 1e3,
-                        "layout": (f"scoring on {kept} of {kept + a.comm_cus} CUs (CU-masked stream), " if kept else
+                        "layout": ((f"scoring on {kept} of {kept + a.comm_cus} CUs (CU-masked stream), "
+                                    if a.comm_layout == "mask" else
+                                    f"scorer grid {2 * kept} (two workgroups on {kept} CUs' worth), ") if kept else
                                    "scoring on every CU, ") +
                                   ((f"pack on the exchange's stream ({a.comm_cus} CUs)" if kept else
                                     "pack on the exchange's stream") if pack_on_comm else
@@ -578,8 +586,10 @@ def main():
                                comm=cstream)
         finally:
             masked(False)
-        ov["layout"] = (f"scoring + pack on {kept} CUs (CU-masked stream), copy on the other {a.comm_cus}"
-                        if kept else "scoring and exchange on every CU")
+        ov["layout"] = ((f"scoring + pack on {kept} CUs (CU-masked stream), copy on the other {a.comm_cus}"
+                         if a.comm_layout == "mask" else
+                         f"scorer grid {2 * kept}, copy on a second stream") if kept else
+                        "scoring and exchange on every CU")
         # for comparison: one unmasked stream each (the copy then competes
         # for the CUs the persistent scorer holds)
         ov["unmasked"] = {k: v for k, v in overlap_proxy(

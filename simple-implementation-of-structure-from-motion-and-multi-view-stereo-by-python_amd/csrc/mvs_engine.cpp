@@ -397,32 +397,36 @@ struct mvs_ctx {
     size_t ev_used = 0;
     const char* timed_name = "";   // the kernel the last timed pair bracketed
     // The context's scratch (tiled-scorer counters and lists, host-pointer
-    // buffers) may be used on any stream a *_device call names: every use
-    // waits for the previous one (an event on the stream that used it last).
-    hipEvent_t scratch_ev = nullptr;
-    hipStream_t scratch_s = nullptr;
-    // the same for the exchange pack's status words and ticket
+    // buffers) and the exchange pack's status words may be used on any stream
+    // a *_device call names: a call waits for the previous use when the
+    // stream changes.  The event is recorded then, lazily, on the stream that
+    // used the area last (its later work is waited for too): consecutive
+    // calls on one stream enqueue nothing, where an event record after every
+    // call cost the stream ~5 us of idle time before the next call's first
+    // kernel (profiles/r05/r5d_kernel_trace.csv).  A stream destroyed since
+    // its use cannot take the record: the whole device is synchronised then.
     struct StreamOrder {
         hipEvent_t ev = nullptr;
         hipStream_t s = nullptr;
+        bool used = false;
         void acquire(hipStream_t cur) {
-            if (s && s != cur) HIPCHK(hipStreamWaitEvent(cur, ev, 0));
+            if (!used || s == cur) return;
+            if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            if (hipEventRecord(ev, s) != hipSuccess) {
+                (void)hipGetLastError();
+                HIPCHK(hipDeviceSynchronize());
+                return;
+            }
+            HIPCHK(hipStreamWaitEvent(cur, ev, 0));
         }
         void release(hipStream_t cur) {
-            if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            HIPCHK(hipEventRecord(ev, cur));
             s = cur;
+            used = true;
         }
-    } pack_order;
+    } scratch_order, pack_order;
     std::string err;
-    void scratch_acquire(hipStream_t s) {
-        if (scratch_s && scratch_s != s) HIPCHK(hipStreamWaitEvent(s, scratch_ev, 0));
-    }
-    void scratch_release(hipStream_t s) {
-        if (!scratch_ev) HIPCHK(hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(scratch_ev, s));
-        scratch_s = s;
-    }
+    void scratch_acquire(hipStream_t s) { scratch_order.acquire(s); }
+    void scratch_release(hipStream_t s) { scratch_order.release(s); }
     // next event pair while timing is on, else nulls
     void next_events(hipEvent_t* e0, hipEvent_t* e1) {
         *e0 = *e1 = nullptr;
@@ -1420,12 +1424,12 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
 void mvs_ctx_destroy(mvs_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->scratch_ev) (void)hipEventSynchronize(ctx->scratch_ev);
-    if (ctx->pack_order.ev) (void)hipEventSynchronize(ctx->pack_order.ev);
+    // the scratch's last users may be any streams (some perhaps destroyed by now)
+    if (ctx->scratch_order.used || ctx->pack_order.used) (void)hipDeviceSynchronize();
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
-    if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
+    if (ctx->scratch_order.ev) (void)hipEventDestroy(ctx->scratch_order.ev);
     if (ctx->pack_order.ev) (void)hipEventDestroy(ctx->pack_order.ev);
     delete ctx;
 }

@@ -33,7 +33,9 @@ python -c "
 import csv
 for r in csv.DictReader(open('gpurun_out/${T}_kernel_stats.csv')):
     print('%-60s %6s %9.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs']) / 1e3))" | head -14
-timeout -k 10 600 python -u bench.py --no-stage --no-ring > gpurun_out/${T}_bench_full.log 2>&1 || { tail -5 gpurun_out/${T}_bench_full.log; exit 1; }
+for lay in mask grid; do
+timeout -k 10 600 python -u bench.py --no-stage --no-ring --no-cpu-baseline --secondary-wid 0 --comm-layout $lay > gpurun_out/${T}_bench_$lay.log 2>&1 || { tail -5 gpurun_out/${T}_bench_$lay.log; exit 1; }
 python -c "
-import json; d=json.loads(open('gpurun_out/${T}_bench_full.log').read().strip().splitlines()[-1])
-print(json.dumps(d['exchange'].get('overlap_proxy'), indent=1)); print(json.dumps(d['scaling_baseline']))"
+import json; d=json.loads(open('gpurun_out/${T}_bench_$lay.log').read().strip().splitlines()[-1])
+print('$lay', json.dumps(d['exchange'].get('overlap_proxy'))); print(json.dumps(d['scaling_baseline']))"
+done
