@@ -59,8 +59,9 @@ PEAK_I8 = 5.0e15           # dense i8 MFMA ops/s (2x the 2.5 PF dense bf16; no s
 SIMDS = 1024               # 256 CUs x 4 SIMDs
 CLOCK = 2.4e9              # peak engine clock, Hz
 PMC_PATH = os.path.join(REPO, "profiles", "r04", "pmc.json")
-# kernel / score-call timing: HIP and torch events on every TIME_EVERY-th timed step
-TIME_EVERY = 5
+# kernel / score-call timing: HIP and torch events on every TIME_EVERY-th timed
+# step (the records cost the stream a few us each: sampled, not every step)
+TIME_EVERY = 10
 
 
 def logical_bytes(V, wid):
@@ -323,7 +324,7 @@ def main():
     ap.add_argument("--comm-cus", type=int, default=16,
                     help="N > 1 (and the N = 1 with-pack baseline): CUs left to the all-gather's kernel "
                          "(0: none)")
-    ap.add_argument("--comm-layout", choices=["mask", "grid"], default="mask",
+    ap.add_argument("--comm-layout", choices=["mask", "grid"], default="grid",
                     help="how --comm-cus are kept free: a CU-masked scoring stream (mask) or the "
                          "persistent scorer's grid at two workgroups per remaining CU (grid)")
     ap.add_argument("--pack-on-comm", action="store_true",

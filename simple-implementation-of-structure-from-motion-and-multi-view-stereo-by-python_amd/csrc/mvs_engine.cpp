@@ -435,7 +435,9 @@ struct mvs_ctx {
         if (ev_used + 2 > ev.size()) {
             for (int k = 0; k < 2; ++k) {
                 hipEvent_t e;
-                HIPCHK(hipEventCreate(&e));
+                // no system-scope fence at the record: no L2 writeback between
+                // the timed kernels (the timestamps need none)
+                HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
                 ev.push_back(e);
             }
         }

@@ -175,6 +175,15 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #endif
 // MVS_TAB_SPLIT (A/B switch, mvs_internal.h): measured slower, 120 vs 106 us
 // per 2^20 (profiles/r05/r5c_ab_split_implicit.log)
+// MVS_TAB_TR (A/B switch): the MFMA's operands swapped, so that lane (kh, m)
+// holds candidate m's window products for views 16 nb + 4 kh + r: each lane
+// decides for its own candidate, gathers its table entries as 8- and 32-byte
+// runs (3 loads per view block instead of 8), builds its part of the mask
+// word in a register, and four-lane permlane swaps finish mask, sum and
+// guard (no v_writelane, no row reduction)
+#ifndef MVS_TAB_TR
+#define MVS_TAB_TR 1
+#endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
@@ -258,6 +267,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     const double* __restrict__ tw = mt.w;
     const float* __restrict__ twf = mt.wf;
     constexpr bool SPLIT = FAST && !LT && MVS_TAB_SPLIT;
+    constexpr bool TR = FAST && !LT && !SPLIT && MVS_TAB_TR;
 
     auto region_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_reg1 : s_reg0; };
     auto cand_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_cand1 : s_cand0; };
@@ -451,11 +461,19 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 }
                 // row 0 of the wave: each candidate's table row, published for
                 // the epilogue's lanes; its own S_a and w_a from the tables
-                int sa_raw[NH];
+                int sa_raw[NH], tixv[NH];
                 double wa_raw[NH];
 #pragma unroll
-                for (int h = 0; h < NH; ++h) { sa_raw[h] = 0; wa_raw[h] = 0.0; }
-                if (kh == 0) {
+                for (int h = 0; h < NH; ++h) { sa_raw[h] = 0; wa_raw[h] = 0.0; tixv[h] = 0; }
+                if constexpr (TR) {
+                    // every lane: its candidate m's table row, S_a and w_a
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        tixv[h] = tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
+                        sa_raw[h] = tsb[tixv[h] + Rv[h]];
+                        wa_raw[h] = tw[tixv[h] + Rv[h]];
+                    }
+                } else if (kh == 0) {
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
                         // LT: element of the pixel inside the staged tile rows
@@ -584,8 +602,12 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         for (int nb = 0; nb < NBLK; ++nb) {
                             const v4i B = {(int)bv[cs][nb].x, (int)bv[cs][nb].y, (int)bv[cs][nb].z, (int)bv[cs][nb].w};
 #pragma unroll
-                            for (int h = 0; h < NH; ++h)
-                                C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[h], B, C[h][nb], 0, 0, 0);
+                            for (int h = 0; h < NH; ++h) {
+                                if constexpr (TR)   // C[h][nb] = views x candidates
+                                    C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B, A[h], C[h][nb], 0, 0, 0);
+                                else
+                                    C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[h], B, C[h][nb], 0, 0, 0);
+                            }
                         }
                         __builtin_amdgcn_sched_barrier(0);
                     }
@@ -604,6 +626,114 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 }
                 TSTAMP(tk1);
                 TSTAMP_ADD(5, tk1 - tk0);
+                if constexpr (TR) {
+                    // lane (kh, m) holds C[h][nb][r] = block h's candidate m, view
+                    // 16 nb + 4 kh + r: its table entries are 4 consecutive S_b
+                    // (8 B) and w (32 B) of the candidate's pixel row
+                    const int vb = 4 * kh;
+                    uint2 sbq[NH][NBLK];
+                    double2 wq0[NH][NBLK], wq1[NH][NBLK];
+#pragma unroll
+                    for (int h = 0; h < NH; ++h)
+#pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) {
+                            const int o = tixv[h] + 16 * nb + vb;
+                            sbq[h][nb] = *(const uint2*)(tsb + o);
+                            wq0[h][nb] = *(const double2*)(tw + o);
+                            wq1[h][nb] = *(const double2*)(tw + o + 2);
+                        }
+                    const int jl = lane & 31;   // permlane swaps: partner = lane ^ 16, ^ 32
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        const double wa = wa_raw[h];
+                        const float T = valid[h] ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf("");
+                        const float gT = 2e-6f * fabsf(T);
+                        const int Sa = -sa_raw[h];
+                        uint32_t m12 = 0u;
+                        double sum = 0.0;
+                        float mn = __builtin_inff();
+                        // views in descending order: bit 4 nb + r of m12 = view (nb, r)
+                        static_for<NBLK * 4>([&](auto Qc) {
+                            constexpr int q = NBLK * 4 - 1 - (int)Qc;
+                            constexpr int nb = q >> 2, r = q & 3;
+                            const uint32_t wd = (r < 2) ? sbq[h][nb].x : sbq[h][nb].y;
+                            const int sb = (r & 1) ? ((int)wd >> 16) : (int)(int16_t)(wd & 0xffffu);
+                            const int num = __mul24(Sa, sb) + __mul24(NPX, C[h][nb][r]);
+                            const double w = r == 0 ? wq0[h][nb].x : r == 1 ? wq0[h][nb].y : r == 2 ? wq1[h][nb].x : wq1[h][nb].y;
+                            // ncc > thr <=> num w_b > T (module comment); a constant
+                            // window (w_b nan) never passes
+                            const float x = fmaf((float)num, (float)w, -T);
+                            const uint64_t P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);      // ogt
+                            m12 = m12 + m12 + (x > 0.0f ? 1u : 0u);
+                            sum = fma_f64_lanes(sum, num, w, P);
+                            mn = fminf(mn, fabsf(x));
+                        });
+                        // the lane's bits into the candidate's mask words
+                        uint32_t mw[2] = {0u, 0u};
+#pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) mw[nb >> 1] |= ((m12 >> (4 * nb)) & 15u) << (16 * (nb & 1) + vb);
+                        // combine the four lanes of candidate m (kh = 0..3)
+                        auto swap_or = [&](uint32_t x) {
+                            auto r16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+                            x = r16[0] | r16[1];
+                            auto r32 = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+                            return r32[0] | r32[1];
+                        };
+                        auto swap_add = [&](double v) {
+                            const unsigned long long u = __double_as_longlong(v);
+                            auto l16 = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+                            auto h16 = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+                            // the partner's half is the element that differs from this lane's own
+                            const bool lo16 = (jl & 16) == 0;
+                            const double p16 = __longlong_as_double(((unsigned long long)(lo16 ? h16[1] : h16[0]) << 32) |
+                                                                    (lo16 ? l16[1] : l16[0]));
+                            v += p16;
+                            const unsigned long long u2 = __double_as_longlong(v);
+                            auto l32 = __builtin_amdgcn_permlane32_swap((uint32_t)u2, (uint32_t)u2, false, false);
+                            auto h32 = __builtin_amdgcn_permlane32_swap((uint32_t)(u2 >> 32), (uint32_t)(u2 >> 32), false, false);
+                            const bool lo32 = lane < 32;
+                            const double p32 = __longlong_as_double(((unsigned long long)(lo32 ? h32[1] : h32[0]) << 32) |
+                                                                    (lo32 ? l32[1] : l32[0]));
+                            return v + p32;
+                        };
+                        auto swap_min = [&](float v) {
+                            auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                            v = fminf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+                            auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                            return fminf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+                        };
+                        mw[0] = swap_or(mw[0]);
+                        if constexpr (NBLK > 2) mw[1] = swap_or(mw[1]);
+                        const double mine = a.avg != nullptr ? swap_add(sum) : 0.0;
+                        const bool gg = swap_min(mn) < gT;
+                        if (kh == 0 && valid[h]) {
+                            uint64_t mk = (uint64_t)mw[0] | ((uint64_t)mw[1] << 32);
+                            // the reference view itself is no V entry (MVS2.py:66-67)
+                            const uint64_t self = (mk >> Rv[h]) & 1ull;
+                            mk &= ~(1ull << Rv[h]);
+                            const int cnt = __popcll(mk);
+                            const int64_t idx = e[h].x;
+                            double av = 0.0;
+                            if (a.avg) {
+                                // its own term num_RR w_a = D_a w_a = 1 / w_a leaves the sum
+                                double inv = __builtin_amdgcn_rcp(wa);
+                                inv = inv * (2.0 - wa * inv);
+                                const double sm = self ? mine - inv : mine;
+                                av = cnt ? sm * (kn * wa) * s_recip[cnt] : 0.0;
+                            }
+                            if (a.rec) {
+                                const unsigned long long ab = __double_as_longlong(av);
+                                *(uint4*)(a.mask + 2 * idx) = make_uint4((uint32_t)mk, (uint32_t)(mk >> 32), (uint32_t)ab,
+                                                                         (uint32_t)(ab >> 32));
+                            } else {
+                                a.mask[idx] = mk;
+                                a.count[idx] = cnt;
+                                if (a.avg) a.avg[idx] = av;
+                            }
+                            if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
+                        }
+                    }
+                } else {
                 // the first candidate step's table values (issued after the K-loop:
                 // in flight across it they would hold 18 registers)
                 fetch(std::integral_constant<int, 0>{});
@@ -739,6 +869,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         }
                         if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
                     }
+                }
                 }
                 TSTAMP(tk2);
                 TSTAMP_ADD(6, tk2 - tk1);
