@@ -180,9 +180,21 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 // decides for its own candidate, gathers its table entries as 8- and 32-byte
 // runs (3 loads per view block instead of 8), builds its part of the mask
 // word in a register, and four-lane permlane swaps finish mask, sum and
-// guard (no v_writelane, no row reduction)
+// guard (no v_writelane, no row reduction).  Measured slower, 115-117 vs
+// 103.5-104.6 us per 2^20 (profiles/r05/r5e_ab_transposed.log): its first
+// table use waits for the next item's LDS-DMA too (the compiler does not
+// order the two kinds of load, so every such wait is a vmcnt(0)), and the
+// loads issued before the K-loop instead spill at 4 waves per SIMD
 #ifndef MVS_TAB_TR
-#define MVS_TAB_TR 1
+#define MVS_TAB_TR 0
+#endif
+// MVS_TAB_DMA_WAVES (A/B switch): only the last this-many waves issue the next
+// item's LDS-DMA.  A wave's wait for any load issued after a pending LDS-DMA
+// is a vmcnt(0) (the compiler does not order the two kinds), so the waves
+// that issue none never wait for the next item's region at their table
+// gathers; the issuing waves take the DMA's instruction cost
+#ifndef MVS_TAB_DMA_WAVES
+#define MVS_TAB_DMA_WAVES 8
 #endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
@@ -233,7 +245,9 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     constexpr bool DB = TG::DB, LT = TG::LT;
 
     constexpr int RPV = VS / 32;                                          // region rows per view incl. the pad row
-    constexpr int PF = (VP * RPV * 2 + kTabThreads - 1) / kTabThreads;    // 16-B pieces per thread
+    constexpr int DW = MVS_TAB_DMA_WAVES, DT = DW * 64;                   // the DMA's waves and threads
+    static_assert(DW >= 1 && DW <= kTabWaves, "DMA waves");
+    constexpr int PF = (VP * RPV * 2 + DT - 1) / DT;                      // 16-B pieces per DMA thread
     constexpr int RB = TG::RB, CB = TG::CB;
     // distinct LDS objects per buffer: reads of one do not wait for the
     // LDS-DMA into the other; each region buffer ends in 16 zero bytes (rows
@@ -274,18 +288,20 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     auto tab_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_tab1 : s_tab0; };
     // the item's region (gv rows) and sorted (id, pk) entries by LDS-DMA
     auto stage = [&](const int4 d, auto bufc) {
+        if (wave < kTabWaves - DW) return;                 // not one of the DMA's waves
+        const int wd = wave - (kTabWaves - DW), td = tid - (kTabWaves - DW) * 64;
         const int ty = d.x / t.ntx, tx = d.x - ty * t.ntx;
         const int x0 = tx * MVS_TILE_W, yr0 = ty * MVS_TILE_H - WID;
         uint8_t* base = region_buf(bufc);
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
-            const int k = opaque(tid) + p * kTabThreads;   // recomputed per piece: no long-lived offsets
+            const int k = opaque(td) + p * DT;   // recomputed per piece: no long-lived offsets
             if (k < npiece) {
                 const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
                 const int y = min(max(yr0 + (r2 >> 1), 0), sc.H - 1);
                 const uint8_t* src = sc.gv + ((int64_t)v * sc.H + y) * sc.Wp + (x0 - 8) + 16 * (r2 & 1);
                 __builtin_amdgcn_global_load_lds((const void*)src,
-                                                 (void __attribute__((address_space(3)))*)(base + (p * kTabThreads + wave * 64) * 16),
+                                                 (void __attribute__((address_space(3)))*)(base + (p * DT + wd * 64) * 16),
                                                  16, 0, 0);
             }
         }
@@ -296,8 +312,8 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
             constexpr int PS = 2 * VP, PD = 4 * VP, NPT = 8 * (PS + PD);   // 16-B pieces
             const int yt0 = ty * MVS_TILE_H;
 #pragma unroll
-            for (int p = 0; p < (NPT + kTabThreads - 1) / kTabThreads; ++p) {
-                const int k = opaque(tid) + p * kTabThreads;
+            for (int p = 0; p < (NPT + DT - 1) / DT; ++p) {
+                const int k = opaque(td) + p * DT;
                 if (k < NPT) {
                     const uint8_t* src;
                     if (k < 8 * PS) {
@@ -310,7 +326,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         src = (const uint8_t*)(mt.d + px * VP) + 16 * c;
                     }
                     __builtin_amdgcn_global_load_lds((const void*)src,
-                                                     (void __attribute__((address_space(3)))*)(tab_buf(bufc) + (p * kTabThreads + wave * 64) * 16),
+                                                     (void __attribute__((address_space(3)))*)(tab_buf(bufc) + (p * DT + wd * 64) * 16),
                                                      16, 0, 0);
                 }
             }
@@ -320,11 +336,11 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         uint8_t* cbase = cand_buf(bufc);
         const uint8_t* csrc = (const uint8_t*)(sorted + d.y);
 #pragma unroll
-        for (int p = 0; p < (kTabChunk / 2 + kTabThreads - 1) / kTabThreads; ++p) {
-            const int k = tid + p * kTabThreads;
+        for (int p = 0; p < (kTabChunk / 2 + DT - 1) / DT; ++p) {
+            const int k = td + p * DT;
             if (k < d.w / 2)
                 __builtin_amdgcn_global_load_lds((const void*)(csrc + 16 * k),
-                                                 (void __attribute__((address_space(3)))*)(cbase + (p * kTabThreads + wave * 64) * 16),
+                                                 (void __attribute__((address_space(3)))*)(cbase + (p * DT + wd * 64) * 16),
                                                  16, 0, 0);
         }
     };
