@@ -196,6 +196,12 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_DMA_WAVES
 #define MVS_TAB_DMA_WAVES 8
 #endif
+// MVS_TAB_DMA_LATE (A/B switch): a wave issues its part of the next item's
+// LDS-DMA after its first unit instead of at the round's start, so that its
+// first unit's table gathers do not wait for the DMA (see above)
+#ifndef MVS_TAB_DMA_LATE
+#define MVS_TAB_DMA_LATE 0
+#endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         // round's end), item k+1's region and list into the other buffer,
         // thread 0's claim of the one after that
         const int4 dst1 = make_int4(it1.x, it1.x * t.cap + it1.y * t.chunk, 0, min(t.chunk, t.cap - it1.y * t.chunk));
-        if constexpr (DB) {
+        if constexpr (DB && !MVS_TAB_DMA_LATE) {
             if (nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
         }
         // unconditional (clamped) loads: no branch, no register reset that
@@ -893,6 +899,12 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
             if (nh == 2) unit(std::integral_constant<int, 2>{});
             else unit(std::integral_constant<int, 1>{});
             TSTAMP_ADD(4, nh);
+            if constexpr (DB && MVS_TAB_DMA_LATE) {
+                if (fb == b0 && nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
+            }
+        }
+        if constexpr (DB && MVS_TAB_DMA_LATE) {
+            if (b0 >= b1 && nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
         }
         TSTAMP(ts3);
         if (wave == 0) TSTAMP_ADD(0, 1);

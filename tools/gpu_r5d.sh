@@ -24,8 +24,10 @@ sb=d['scaling_baseline']
 print('$v rep $rep: %.3f G cand/s  step %.1f us  kernel %.1f us  pack %.1f us  with-pack step %.1f us (%s)' % (d['value']/1e9, d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, d['exchange']['pack_us'], sb['step_ms_with_pack']*1e3, sb['layout']))" | tee -a gpurun_out/${T}_ab.log
   done
 done
-[ -z "$NO_UBENCH" ] && timeout -k 10 120 tools/ubench/bin_atomics > gpurun_out/${T}_bin_atomics.log 2>&1 || { [ -z "$NO_UBENCH" ] && cat gpurun_out/${T}_bin_atomics.log; exit 1; }
-[ -z "$NO_UBENCH" ] && cat gpurun_out/${T}_bin_atomics.log
+if [ -z "$NO_UBENCH" ]; then
+  timeout -k 10 120 tools/ubench/bin_atomics > gpurun_out/${T}_bin_atomics.log 2>&1 || { cat gpurun_out/${T}_bin_atomics.log; exit 1; }
+  cat gpurun_out/${T}_bin_atomics.log
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python bench.py $B > gpurun_out/${T}_prof.log 2>&1 || { tail -5 gpurun_out/${T}_prof.log; exit 1; }
 f=$(find gpurun_out/prof_$T -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/${T}_kernel_stats.csv
 f=$(find gpurun_out/prof_$T -name '*kernel_trace.csv' | head -1); cp "$f" gpurun_out/${T}_kernel_trace.csv; rm -rf gpurun_out/prof_$T
