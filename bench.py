@@ -18,7 +18,7 @@ Beside the headline (rank 0 at N = 1 only, so that the driver's N > 1 runs
 stay short):
   roofline     the binding roof of the dominant kernel (k_score_mma) from the
                live kernel time and the per-launch counters of the committed
-               rocprofv3 PMC profile (profiles/r04/pmc.json): HBM bytes,
+               rocprofv3 PMC profile (profiles/r05/pmc.json): HBM bytes,
                VALU-busy cycles, MFMA i8 operations; frac <= 1 each
   cold_sweep   scene setup from the resident images (k_build_scene) + the sweep
   secondary    wid 3 (BASELINE config 2's 7x7 window)
@@ -58,7 +58,7 @@ PEAK_HBM = 8.0e12          # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
 PEAK_I8 = 5.0e15           # dense i8 MFMA ops/s (2x the 2.5 PF dense bf16; no sparsity)
 SIMDS = 1024               # 256 CUs x 4 SIMDs
 CLOCK = 2.4e9              # peak engine clock, Hz
-PMC_PATH = os.path.join(REPO, "profiles", "r04", "pmc.json")
+PMC_PATH = os.path.join(REPO, "profiles", "r05", "pmc.json")
 # kernel / score-call timing: HIP and torch events on every TIME_EVERY-th timed
 # step (the records cost the stream a few us each: sampled, not every step)
 TIME_EVERY = 10
