@@ -193,7 +193,10 @@ struct ExpandArgs {
 #define MVS_MMA_CHUNK 1024    // candidates per work item, V <= 64 (whole tiles, as a rule)
 #define MVS_GROUP_VIEWS 64    // views per group when V > 64
 #define MVS_GROUP_CHUNK 116   // candidates per work item when V > 64 (their reference rows staged)
-#define MVS_ACC_CHUNK 2048    // candidates per chunk of the exchange's pack (k_acc_pack)
+#ifndef MVS_ACC_PER
+#define MVS_ACC_PER 8         // candidates per thread of the exchange's pack (A/B switch)
+#endif
+#define MVS_ACC_CHUNK (256 * MVS_ACC_PER)   // candidates per chunk of the exchange's pack (k_acc_pack)
 
 extern "C" {
 // RGB -> stack and gv (one pass, coalesced on both sides); the caller zeroes

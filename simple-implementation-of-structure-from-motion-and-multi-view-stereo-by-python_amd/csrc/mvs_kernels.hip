@@ -2052,7 +2052,7 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 // accepted candidates' points as soon as the counts are in; they stay in
 // flight across the chunk's scan and look-back (LDS-only barriers), so that
 // the rows go out as soon as the prefix is in.
-constexpr int kAccThreads = 256, kAccPer = 8, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
+constexpr int kAccThreads = 256, kAccPer = MVS_ACC_PER, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
 constexpr int kAccE = kAccPer * kAccWaves;          // (j, wave) counts of a chunk
 constexpr int kAccEpl = (kAccE + 63) / 64;          // of them per lane of wave 0's scan
 constexpr int kAccLB = 8;                            // status words per lane of the look-back window

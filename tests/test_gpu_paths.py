@@ -344,12 +344,13 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
 
 @pytest.mark.parametrize("n", [1, 2047, 2049, 200_001, 5_000_001])
 def test_pack_accepted_lookback_sizes(pkg, ctx, n):
-    """The pack's one-launch look-back over 2,048-candidate chunks: a single
-    partial chunk, a chunk boundary, several look-back windows (98 chunks at
-    200k), and more chunks (2,442 at 5M) than workgroups (2,048), so
-    workgroups take a second chunk whose predecessors belong to other
-    workgroups; synthetic counts/masks against the torch reference, twice in
-    a row (the status words' epoch changes between calls)."""
+    """The pack's one-launch look-back over 2,048-candidate chunks (one
+    workgroup each): a single partial chunk, a chunk boundary, several
+    look-back windows (98 chunks at 200k), and more chunks (2,442 at 5M) than
+    workgroups resident at once, so that chunks wait on predecessors
+    dispatched in earlier rounds; synthetic counts/masks against the torch
+    reference, twice in a row (the status words' epoch changes between
+    calls)."""
     import importlib
     import torch
     par = importlib.import_module(pkg.__name__ + ".parallel")
