@@ -77,7 +77,15 @@ int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int 
  * Calls on different streams are ordered too: a call waits for the previous
  * call's use of the context's scratch (an event on that call's stream).
  * d_avg may be NULL when avg_ncc_score is not needed (it only feeds the
- * disabled filter_out_outlier, MVS2.py:281). */
+ * disabled filter_out_outlier, MVS2.py:281).
+ * Device memory: the first tiled call with a given wid builds that wid's
+ * window-moment tables, kept for the context's life: (H*W + 16) * VP
+ * entries (VP = V rounded up to 16, or to 64 at V > 64) of 10 B at
+ * V <= 64 (S_b int16 + w binary64) or 6 B at V > 64 (S_b int16 + D int32)
+ * -- 147 MB per wid for dinoRing (48 x 640 x 480), 3.2 GB for
+ * 256 x 1920 x 1080.  Past 2^31
+ * entries, or when the allocation fails, that scene is scored with the
+ * in-kernel moments instead (same results, slower). */
 int mvs_score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_ref, int wid,
                      double min_ncc, double* d_xy, uint64_t* d_mask, int32_t* d_count,
                      double* d_avg, void* stream);

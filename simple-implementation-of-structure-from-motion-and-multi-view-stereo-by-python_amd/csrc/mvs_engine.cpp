@@ -342,8 +342,8 @@ struct mvs_ctx {
         m.wid = wid;
         return m;
     }
-    // the tables of wid (6 B per (pixel, view): S_b and D; 10 B at 48 < V <=
-    // 64: S_b and w), built on stream s if needed; false when they do not
+    // the tables of wid (10 B per (pixel, view) at V <= 64: S_b and w; 6 B at
+    // V > 64 or V <= MVS_TAB_LT_VIEWS: S_b and D), built on stream s if needed; false when they do not
     // apply (disabled, or more than 2^31 elements).  One row of 16 pixels
     // past the end: k_score_tab stages a tile's rows whole (16 pixels x VP),
     // also where the last tile column runs past W
