@@ -28,13 +28,22 @@ if [ -z "$NO_UBENCH" ]; then
   timeout -k 10 120 tools/ubench/bin_atomics > gpurun_out/${T}_bin_atomics.log 2>&1 || { cat gpurun_out/${T}_bin_atomics.log; exit 1; }
   cat gpurun_out/${T}_bin_atomics.log
 fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o run --output-format csv -- python bench.py $B > gpurun_out/${T}_prof.log 2>&1 || { tail -5 gpurun_out/${T}_prof.log; exit 1; }
-f=$(find gpurun_out/prof_$T -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/${T}_kernel_stats.csv
-f=$(find gpurun_out/prof_$T -name '*kernel_trace.csv' | head -1); cp "$f" gpurun_out/${T}_kernel_trace.csv; rm -rf gpurun_out/prof_$T
+# rocprof kernel stats of the main library (PROF_VARIANTS=1: of every variant, twice)
+PV=main; PR=1; [ -n "$PROF_VARIANTS" ] && { PV="main ${VARIANTS}"; PR="1 2"; }
+for rep in $PR; do
+for v in $PV; do
+L=$L0; [ $v != main ] && L=${L0%.so}_$v.so
+S=$T; [ $v != main ] && S=${T}_$v
+MVS_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$S -o run --output-format csv -- python bench.py $B > gpurun_out/${S}_prof.log 2>&1 || { tail -5 gpurun_out/${S}_prof.log; exit 1; }
+f=$(find gpurun_out/prof_$S -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/${S}_kernel_stats.csv
+f=$(find gpurun_out/prof_$S -name '*kernel_trace.csv' | head -1); cp "$f" gpurun_out/${S}_kernel_trace.csv; rm -rf gpurun_out/prof_$S
+echo "== $v (rocprof, rep $rep)"
 python -c "
 import csv
-for r in csv.DictReader(open('gpurun_out/${T}_kernel_stats.csv')):
-    print('%-60s %6s %9.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs']) / 1e3))" | head -14
+for r in csv.DictReader(open('gpurun_out/${S}_kernel_stats.csv')):
+    print('%-60s %6s %9.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs']) / 1e3))" | head -8 | tee -a gpurun_out/${T}_ab.log
+done
+done
 for lay in ${LAYOUTS-mask grid}; do
 timeout -k 10 600 python -u bench.py --no-stage --no-ring --no-cpu-baseline --secondary-wid 0 --comm-layout $lay > gpurun_out/${T}_bench_$lay.log 2>&1 || { tail -5 gpurun_out/${T}_bench_$lay.log; exit 1; }
 python -c "
