@@ -62,6 +62,18 @@ DEV int opaque(int x) {
 // acc += num * w in the lanes of P only (binary64): EXEC narrowed to P for
 // the conversion and the fma, restored after -- two vector instructions, no
 // select of the term (the compiler's form of the select costs four)
+// the same on a binary64 num (converted once, shared with the decision)
+DEV double fma_f64_lanes_d(double acc, double num, double w, uint64_t P) {
+    uint64_t save;
+    asm volatile(
+        "s_and_saveexec_b64 %[save], %[p]\n\t"
+        "v_fma_f64 %[acc], %[num], %[w], %[acc]\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [acc] "+v"(acc), [save] "=&s"(save)
+        : [num] "v"(num), [w] "v"(w), [p] "s"(P)
+        : "scc");   // EXEC is restored before the statement ends
+    return acc;
+}
 DEV double fma_f64_lanes(double acc, int num, double w, uint64_t P) {
     double t;
     uint64_t save;

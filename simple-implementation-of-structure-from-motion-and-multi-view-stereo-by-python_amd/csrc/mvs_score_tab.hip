@@ -202,6 +202,26 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_DMA_LATE
 #define MVS_TAB_DMA_LATE 0
 #endif
+#ifndef MVS_TAB_WHATIF
+#define MVS_TAB_WHATIF 0
+#endif
+// MVS_TAB_D64 (A/B switch): the FAST decision in binary64 -- x = fma(num,
+// w_b, -T) on the exact num (one conversion shared with the sum) instead of
+// binary32 copies of num and w_b: 8 VALU per (candidate, view) instead of 10.
+// Outside the guard band both decide as exact arithmetic does (108 GPU tests
+// green with it).  Measured no faster: 104.9-106.1 vs 103.4-106.5 us, with
+// MAXSUM 108.0-108.3 (profiles/r05/r5k_*, r5l_*); the what-if builds
+// (MVS_TAB_WHATIF) put the table gathers at ~11 % of the scorer's time
+#ifndef MVS_TAB_D64
+#define MVS_TAB_D64 0
+#endif
+// MVS_TAB_MAXSUM (with D64): the passing terms summed as max(x, 0), and
+// (passing views) x T added once per candidate: num w_b = x + T for a
+// passing pair up to one rounding of x (well inside avg's 1e-12), with no
+// EXEC change per (candidate, view)
+#ifndef MVS_TAB_MAXSUM
+#define MVS_TAB_MAXSUM 1
+#endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
@@ -211,9 +231,20 @@ constexpr int kTabChunk = MVS_MMA_CHUNK;
 struct alignas(16) TabInfo {
     int32_t tix;   // table element of its pixel, view 0
     int32_t Sa;    // -S_a
+#if MVS_TAB_D64
+    double T;      // FAST: decision threshold on num w_b; else the reference view (-1: no candidate)
+#else
     int32_t R;     // reference view (-1: no candidate)
     float T;       // decision threshold on num w_b (FAST)
+#endif
 };
+#if MVS_TAB_D64
+DEV void ti_set_R(TabInfo& t, int R) { t.T = (double)R; }
+DEV int ti_R(const TabInfo& t) { return (int)t.T; }
+#else
+DEV void ti_set_R(TabInfo& t, int R) { t.R = R; }
+DEV int ti_R(const TabInfo& t) { return t.R; }
+#endif
 
 template <int WID, int NBLK>
 struct TabGeom {
@@ -276,6 +307,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
+    const double tqd = a.thr / kn;
     ItemMap im;
     im.load(t);
     // implicit items: k < ntiles is (tile k, chunk 0), then segment 1's
@@ -501,7 +533,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         // LT: element of the pixel inside the staged tile rows
                         const int tix = LT ? (rrel[h] * MVS_TILE_W + qrel[h]) * VP : tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
                         ti[16 * h + m].tix = tix;
-                        ti[16 * h + m].R = valid[h] ? Rv[h] : -1;
+                        if constexpr (!FAST || !MVS_TAB_D64) ti_set_R(ti[16 * h + m], valid[h] ? Rv[h] : -1);
                         if constexpr (LT) {
                             sa_raw[h] = ls_sb[tix + Rv[h]];
                             wa_raw[h] = w_of(ls_d[tix + Rv[h]]);
@@ -538,8 +570,12 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                                 sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
                                 wfv[i & 1][h][nb] = twf[tix + 16 * nb];
                             } else {
-                                sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
-                                wv[i & 1][h][nb] = tw[tix + 16 * nb];
+                                // MVS_TAB_WHATIF (measurement only, wrong results): bit 0
+                                // drops the w gathers, bit 1 the S_b gathers
+                                if constexpr (MVS_TAB_WHATIF & 2) sbv[i & 1][h][nb] = tix & 255;
+                                else sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
+                                if constexpr (MVS_TAB_WHATIF & 1) wv[i & 1][h][nb] = 1e-3 * (double)(tix & 1023);
+                                else wv[i & 1][h][nb] = tw[tix + 16 * nb];
                             }
                         }
                     }
@@ -768,10 +804,15 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                     for (int h = 0; h < NH; ++h) {
                         const double wa = wa_raw[h];
                         ti[16 * h + m].Sa = -sa_raw[h];
-                        // FAST: T = thr (n-1)/n sqrt(da) in binary32 (1-ulp reciprocal,
-                        // well inside the guard band); else the decision is on ncc
+                        // FAST: T = thr (n-1)/n sqrt(da) (binary32: a 1-ulp reciprocal;
+                        // binary64: a correctly rounded quotient; both well inside the
+                        // guard band); else the decision is on ncc
+#if MVS_TAB_D64
+                        if constexpr (FAST) ti[16 * h + m].T = valid[h] ? tqd / wa : __builtin_nan("");
+#else
                         ti[16 * h + m].T = FAST ? (valid[h] ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf(""))
                                                 : 0.0f;
+#endif
                         my_wa[h] = wa;
                     }
                 }
@@ -787,12 +828,18 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
                         const TabInfo c = ti[16 * h + 4 * kh + i];
+#if MVS_TAB_D64
+                        const double gT = 2e-6 * fabs(c.T);
+                        double ax[NBLK];
+#else
                         const float gT = 2e-6f * fabsf(c.T);
+                        float ax[NBLK];
+#endif
                         double ca = 0.0;
-                        if constexpr (!FAST) ca = c.R < 0 ? 0.0 : kn * (LT ? w_of(ls_d[c.tix + c.R]) : tw[c.tix + c.R]);
+                        const int cR = ti_R(c);
+                        if constexpr (!FAST) ca = cR < 0 ? 0.0 : kn * (LT ? w_of(ls_d[c.tix + cR]) : tw[c.tix + cR]);
                         double sa = 0.0;
                         uint64_t g = 0;
-                        float ax[NBLK];
                         static_for<NBLK>([&](auto Nc) {
                             constexpr int nb = Nc;
                             const int vl = 16 * nb + m;
@@ -814,26 +861,42 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                                 // never passes.  The candidate's own view R passes (its ncc
                                 // is n/(n-1) > thr): its mask bit and its term of the sum
                                 // are taken out once per candidate
+#if MVS_TAB_D64
+                                const double numd = (double)num;
+                                const double x = fma(numd, w, -c.T);
+                                P = __builtin_amdgcn_fcmp(x, 0.0, 2);                           // ogt
+                                ax[nb] = x;
+                                if constexpr (MVS_TAB_MAXSUM) sa += fmax(x, 0.0);   // a nan x adds 0
+                                else sa = fma_f64_lanes_d(sa, numd, w, P);
+#else
                                 const float x = fmaf((float)num, (float)w, -c.T);
                                 P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
                                 ax[nb] = x;
                                 sa = fma_f64_lanes(sa, num, w, P);
+#endif
                             } else {
                                 const double w = wv[i & 1][h][nb];
                                 const double ncc = (double)num * w * ca;
-                                const bool pass = vl != c.R && ncc > a.thr;
+                                const bool pass = vl != cR && ncc > a.thr;
                                 P = __ballot(pass);
-                                g |= __ballot(vl != c.R && fabs(ncc - a.thr) <= kGuard);
+                                g |= __ballot(vl != cR && fabs(ncc - a.thr) <= kGuard);
                                 sa = fma((double)num, pass ? w : 0.0, sa);
                             }
                             pmv[h] = writelane<2 * (i * NBLK + nb)>(pmv[h], (uint32_t)P);
                             pmv[h] = writelane<2 * (i * NBLK + nb) + 1>(pmv[h], (uint32_t)(P >> 32));
                         });
                         if constexpr (FAST) {
+#if MVS_TAB_D64
+                            double mn = fabs(ax[0]);
+#pragma unroll
+                            for (int nb = 1; nb < NBLK; ++nb) mn = fmin(mn, fabs(ax[nb]));
+                            g = __builtin_amdgcn_fcmp(mn, gT, 4);                                // olt
+#else
                             float mn = fabsf(ax[0]);
 #pragma unroll
                             for (int nb = 1; nb < NBLK; ++nb) mn = fminf(mn, fabsf(ax[nb]));
                             g = __builtin_amdgcn_fcmpf(mn, gT, 4);                               // olt
+#endif
                         }
                         gdv[h] = writelane<2 * i>(gdv[h], (uint32_t)g);
                         gdv[h] = writelane<2 * i + 1>(gdv[h], (uint32_t)(g >> 32));
@@ -873,6 +936,10 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         const int64_t idx = e[h].x;
                         double av = 0.0;
                         if (a.avg) {
+#if MVS_TAB_D64 && MVS_TAB_MAXSUM
+                            // the passing terms' T (see MVS_TAB_MAXSUM)
+                            if constexpr (FAST) mine += (double)(cnt + (int)self) * ti[16 * h + m].T;
+#endif
                             // its own term num_RR w_a = D_a w_a = 1 / w_a leaves the sum
                             double inv = __builtin_amdgcn_rcp(my_wa[h]);
                             inv = inv * (2.0 - my_wa[h] * inv);
