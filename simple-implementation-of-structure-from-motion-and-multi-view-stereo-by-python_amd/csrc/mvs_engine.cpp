@@ -307,6 +307,7 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand;
+    DevBuf<int32_t> t_bin;   // MVS_BIN3: binning workgroups' tile histograms + per-candidate words
     // mvs_pack_accepted: the chunks' look-back words (one per MVS_ACC_CHUNK
     // candidates), their epoch and the give-up counter
     DevBuf<uint64_t> p_status;
@@ -576,6 +577,15 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.item_seg = (int)(n / std::max(t.chunk, 1) + ntiles + 2);
         ctx->t_items.ensure((size_t)kItemSegs * t.item_seg);
         t.items = ctx->t_items.p;
+        if (MVS_BIN3 && ntiles <= 16384) {
+            // one histogram row per binning workgroup, then an int2 per candidate
+            const int64_t nbin = (n + MVS_BIN_CHUNK - 1) / MVS_BIN_CHUNK;
+            const int64_t rows = (nbin * ntiles + 1) & ~(int64_t)1;
+            ctx->t_bin.ensure((size_t)(rows + 2 * n));
+            t.bin_rows = ctx->t_bin.p;
+            t.bin_scratch = (int2*)(ctx->t_bin.p + rows);
+            t.bin_words = rows + 2 * n;
+        }
         t.zero_first = ctx->tiles_clean_ntiles != ntiles ? 1 : 0;
         t.grid = ctx->scorer_wgs;
         ctx->tiles_clean_ntiles = -1;            // dirty until the sequence is queued

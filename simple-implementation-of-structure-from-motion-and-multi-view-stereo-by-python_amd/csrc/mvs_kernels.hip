@@ -312,9 +312,7 @@ __global__ __launch_bounds__(256) void k_score(const SceneDev sc, const ScoreArg
 // order; the scorers read the tile's final count when they take the item
 // (item_desc).
 // ---------------------------------------------------------------------------
-#ifndef MVS_BIN_PER
-#define MVS_BIN_PER 4   // candidates per k_bin thread (A/B switch)
-#endif
+// MVS_BIN_PER (mvs_internal.h): candidates per k_bin thread (A/B switch)
 #ifdef MVS_STAMPS
 // diagnostic build only: per-workgroup cycle sums of the scorer's phases
 // (slot 0 items, 1 staging + barrier, 2 moments, 3 candidates, 4 wave 0's own
@@ -343,6 +341,8 @@ __device__ unsigned long long g_stamps[4096 * 16];
 #endif
 
 constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
+static_assert(kBinBlock * kBinPer == MVS_BIN_CHUNK, "the host sizes bin_rows by MVS_BIN_CHUNK");
+static_assert(kBinBlock * kBinPer <= 4096, "k_bin_count packs a rank inside the workgroup into 12 bits");
 #ifndef MVS_IMPLICIT_MEAN
 #define MVS_IMPLICIT_MEAN 64   // A/B switch (a huge value keeps k_item_scan everywhere)
 #endif
@@ -501,6 +501,136 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     STAMP_ADD_ROW(2048 + blockIdx.x, 1, t1 - t0);
     STAMP_ADD_ROW(2048 + blockIdx.x, 2, t2 - t1);
     STAMP_ADD_ROW(2048 + blockIdx.x, 3, t3 - t2);
+}
+
+// Binning without global atomics (MVS_BIN3), stage 1 of 3: k_bin's
+// projection, window test and LDS ranks; the workgroup's tile histogram goes
+// out as one row (rows[b * ntiles + k]) and each candidate's (tile, rank in
+// the workgroup | pk << 12) to the scratch word (tile -1: no valid window).
+__global__ __launch_bounds__(kBinBlock) void k_bin_count(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
+                                                         int wid) {
+    extern __shared__ int32_t hist[];      // [ntiles]
+    __shared__ double s_cam[MVS_MAX_VIEWS][16];
+    const int words = (sc.V + 63) >> 6;
+    for (int k = threadIdx.x; k < sc.V * 16; k += blockDim.x) {
+        const int v = k >> 4, f = k & 15;
+        const CamDev& cm = sc.cams[v];
+        s_cam[v][f] = f < 9 ? cm.Rp[f] : f < 12 ? cm.t[f - 9] : f == 12 ? cm.fx : f == 13 ? cm.fy : f == 14 ? cm.cx : cm.cy;
+    }
+    for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
+    int Rk[kBinPer];
+    double ck[kBinPer][3];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        const int64_t ii = i < a.n ? i : 0;
+        Rk[k] = a.ref[ii];
+        ck[k][0] = a.c[3 * ii];
+        ck[k][1] = a.c[3 * ii + 1];
+        ck[k][2] = a.c[3 * ii + 2];
+    }
+    int tl[kBinPer], lr[kBinPer], pk[kBinPer];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        tl[k] = -1;
+        lr[k] = pk[k] = 0;
+        if (i >= a.n) continue;
+        const int R = Rk[k];
+        const double c[3] = {ck[k][0], ck[k][1], ck[k][2]};
+        double px, py;
+        project_vals(s_cam[R], c, px, py);
+        a.xy[2 * i] = px;
+        a.xy[2 * i + 1] = py;
+        int q, r;
+        if (!window_ok(sc, px, py, wid, &q, &r)) {
+            for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
+            if (a.count) a.count[i] = 0;
+            if (a.avg) a.avg[i * a.astride] = 0.0;
+            continue;
+        }
+        const int tx = q / MVS_TILE_W, ty = r / MVS_TILE_H;
+        tl[k] = ty * t.ntx + tx;
+        pk[k] = (q - tx * MVS_TILE_W) | ((r - ty * MVS_TILE_H) << 4) | (R << 7);
+        lr[k] = atomicAdd(&hist[tl[k]], 1);
+    }
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        if (i < a.n) t.bin_scratch[i] = make_int2(tl[k], lr[k] | (pk[k] << 12));
+    }
+    __syncthreads();
+    int32_t* row = t.bin_rows + (int64_t)blockIdx.x * t.ntiles;
+    for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) row[b] = hist[b];
+}
+
+// Stage 2 of 3: 64 tiles per workgroup, each tile's column of nbin counts in
+// 16 segments (one wave each); rows become every workgroup's first slot in
+// the tile's bucket, and the tile's total its count.  Implicit items: the
+// tile's chunks j >= 1 below cap are appended to segment 1.
+constexpr int kBinScanSegs = 16;
+__global__ __launch_bounds__(1024) void k_bin_scan(const TiledArgs t, int nbin) {
+    __shared__ int s_seg[kBinScanSegs][65];
+    const int tl = threadIdx.x & 63, sg = threadIdx.x >> 6;
+    const int tile = blockIdx.x * 64 + tl;
+    const int per = (nbin + kBinScanSegs - 1) / kBinScanSegs;
+    const int w0 = min(sg * per, nbin), w1 = min(w0 + per, nbin);
+    int32_t* col = t.bin_rows + tile;
+    int s = 0;
+    if (tile < t.ntiles) {
+        int w = w0;
+        for (; w + 4 <= w1; w += 4)
+            s += col[(int64_t)w * t.ntiles] + col[(int64_t)(w + 1) * t.ntiles] + col[(int64_t)(w + 2) * t.ntiles] +
+                 col[(int64_t)(w + 3) * t.ntiles];
+        for (; w < w1; ++w) s += col[(int64_t)w * t.ntiles];
+    }
+    s_seg[sg][tl] = s;
+    __syncthreads();
+    int pre = 0;
+    for (int q = 0; q < sg; ++q) pre += s_seg[q][tl];
+    if (tile >= t.ntiles) return;
+    for (int w = w0; w < w1; ++w) {
+        const int c = col[(int64_t)w * t.ntiles];
+        col[(int64_t)w * t.ntiles] = pre;
+        pre += c;
+    }
+    if (sg == kBinScanSegs - 1) {
+        const int total = pre;   // the last segment's prefix after its own: the tile's count
+        t.tile_count[tile * kTcStride] = total;
+        if (t.implicit) {
+            const int end = min(total, t.cap);
+            for (int q = 1; q * t.chunk < end; ++q)
+                t.items[t.item_seg + atomicAdd(&t.n_items[32], 1)] = make_int4(tile, q, 0, 0);
+        }
+    }
+}
+
+// Stage 3 of 3: candidate i of workgroup b goes to its tile's bucket at b's
+// first slot + its rank in b (past the bucket's capacity: the direct path's
+// list), the same entries k_bin writes.
+__global__ __launch_bounds__(kBinBlock) void k_bin_scatter(const ScoreArgs a, const TiledArgs t) {
+    const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
+    const int32_t* row = t.bin_rows + (int64_t)blockIdx.x * t.ntiles;
+    int2 e[kBinPer];
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        e[k] = i < a.n ? t.bin_scratch[i] : make_int2(-1, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        const int tile = e[k].x;
+        if (tile < 0) continue;
+        const int pk = e[k].y >> 12;
+        const int rank = row[tile] + (e[k].y & 4095);
+        if (rank < t.cap)
+            t.sorted[(int64_t)tile * t.cap + rank] = make_int2((int32_t)i, pk);
+        else
+            t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)i, tile, pk, 0);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2500,7 +2630,13 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     // tiles themselves as its items, in tile order, and needs no k_item_scan
     TiledArgs tv = *t;
     tv.implicit = (!grouped && mt && a->n >= (int64_t)kImplicitMean * t->ntiles) ? 1 : 0;
-    if (t->ntiles <= kBinLdsTiles)
+    const bool bin3 = MVS_BIN3 && t->ntiles <= kBinLdsTiles && t->bin_rows && t->bin_scratch &&
+                      (int64_t)nbin * t->ntiles + 2 * a->n <= t->bin_words;
+    if (bin3) {
+        hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, tv, WID);
+        hipLaunchKernelGGL(k_bin_scan, dim3((t->ntiles + 63) / 64), dim3(1024), 0, s, tv, nbin);
+        hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(kBinBlock), 0, s, *a, tv);
+    } else if (t->ntiles <= kBinLdsTiles)
         hipLaunchKernelGGL(k_bin<true>, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, tv, WID);
     else
         hipLaunchKernelGGL(k_bin<false>, dim3(nbin), dim3(kBinBlock), 0, s, *sc, *a, tv, WID);

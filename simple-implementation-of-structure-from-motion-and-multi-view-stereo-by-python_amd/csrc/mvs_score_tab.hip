@@ -307,7 +307,9 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
+#if MVS_TAB_D64
     const double tqd = a.thr / kn;
+#endif
     ItemMap im;
     im.load(t);
     // implicit items: k < ntiles is (tile k, chunk 0), then segment 1's
