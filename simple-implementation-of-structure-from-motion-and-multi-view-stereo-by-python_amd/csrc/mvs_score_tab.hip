@@ -222,6 +222,13 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_MAXSUM
 #define MVS_TAB_MAXSUM 1
 #endif
+// MVS_TAB_TIXV (A/B switch): the table rows of a lane's four candidate steps
+// read as one 16-B LDS load per M-block after the K-loop (a per-wave copy of
+// the tix column), so that no step's gathers wait for an LDS read of their
+// address.  Measured the same: 103.1-105.5 vs 103.3-103.5 us (r5n_*)
+#ifndef MVS_TAB_TIXV
+#define MVS_TAB_TIXV 0
+#endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
@@ -292,6 +299,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB + 16], s_reg1[DB ? RB + 16 : 16];
     __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[DB ? CB : 16];
     __shared__ __attribute__((aligned(16))) TabInfo s_ti[kTabWaves * 32];
+    __shared__ __attribute__((aligned(16))) int32_t s_tix[MVS_TAB_TIXV ? kTabWaves * 32 : 4];
     // LT: the tile's table rows, [S_b rows][D rows]
     __shared__ __attribute__((aligned(16))) uint8_t s_tab0[LT ? TG::TS + TG::TD : 16], s_tab1[LT && DB ? TG::TS + TG::TD : 16];
     __shared__ int s_ids[2];
@@ -535,6 +543,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         // LT: element of the pixel inside the staged tile rows
                         const int tix = LT ? (rrel[h] * MVS_TILE_W + qrel[h]) * VP : tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
                         ti[16 * h + m].tix = tix;
+                        if constexpr (MVS_TAB_TIXV) s_tix[wave * 32 + 16 * h + m] = tix;
                         if constexpr (!FAST || !MVS_TAB_D64) ti_set_R(ti[16 * h + m], valid[h] ? Rv[h] : -1);
                         if constexpr (LT) {
                             sa_raw[h] = ls_sb[tix + Rv[h]];
@@ -550,6 +559,10 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 // the epilogue's table values, one candidate step ahead: lane
                 // (kh, m) needs candidate 4 kh + i's S_b and w_b of views 16 nb + m
                 double sacc[NH][4];
+                if constexpr (MVS_TAB_WHATIF & 8) {
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) sacc[h][0] = sacc[h][1] = sacc[h][2] = sacc[h][3] = 0.0;
+                }
                 int sbv[2][NH][NBLK];
                 double wv[2][NH][NBLK];
                 float wfv[2][NH][NBLK];
@@ -558,11 +571,16 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 int numB[2][NH][NBLK];
                 double wB[2][NH][NBLK];
                 uint64_t PB[2][NH][NBLK];
+                int4 tq[NH];   // MVS_TAB_TIXV: candidates 4 kh + 0..3's table rows
                 auto fetch = [&](auto ic) {
                     constexpr int i = decltype(ic)::value;
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
-                        const int tix = ti[16 * h + 4 * kh + i].tix + m;
+                        int tix;
+                        if constexpr (MVS_TAB_TIXV && !LT)
+                            tix = (i == 0 ? tq[h].x : i == 1 ? tq[h].y : i == 2 ? tq[h].z : tq[h].w) + m;
+                        else
+                            tix = ti[16 * h + 4 * kh + i].tix + m;
 #pragma unroll
                         for (int nb = 0; nb < NBLK; ++nb) {
                             if constexpr (LT) {
@@ -673,7 +691,8 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                     }
                 };
                 using I = std::integral_constant<int, 0>;
-                if (span <= KSK) {
+                if constexpr (MVS_TAB_WHATIF & 4) {   // measurement only: no K-loop
+                } else if (span <= KSK) {
                     kpass(std::integral_constant<int, KSK>{}, std::integral_constant<int, 1>{},
                           std::integral_constant<int, KSK - 2>{}, min(s_lo, KS - KSK), 0);
                 } else if (span == KSK + 1) {
@@ -796,7 +815,11 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 } else {
                 // the first candidate step's table values (issued after the K-loop:
                 // in flight across it they would hold 18 registers)
-                fetch(std::integral_constant<int, 0>{});
+                if constexpr (MVS_TAB_TIXV && !LT) {
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) tq[h] = *(const int4*)(s_tix + wave * 32 + 16 * h + 4 * kh);
+                }
+                if constexpr (!(MVS_TAB_WHATIF & 8)) fetch(std::integral_constant<int, 0>{});
                 // the candidates' decision constants (row 0), now that S_a, w_a are in
                 double my_wa[NH];
 #pragma unroll
@@ -824,6 +847,15 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 uint32_t pmv[NH], gdv[NH];
 #pragma unroll
                 for (int h = 0; h < NH; ++h) pmv[h] = gdv[h] = 0u;
+                if constexpr (MVS_TAB_WHATIF & 8) {   // keep the window products alive (outputs untouched)
+                    int sc_ = 0;
+#pragma unroll
+                    for (int h = 0; h < NH; ++h)
+#pragma unroll
+                        for (int nb = 0; nb < NBLK; ++nb) sc_ += C[h][nb][0] + C[h][nb][1] + C[h][nb][2] + C[h][nb][3];
+                    if (sc_ == 0x7fffffff && a.exact_hits) atomicAdd(a.exact_hits, 1);
+                }
+                if constexpr (!(MVS_TAB_WHATIF & 8))   // measurement only: no decisions
                 static_for<4>([&](auto Ic) {
                     constexpr int i = Ic;
                     if constexpr (i < 3) fetch(std::integral_constant<int, i + 1>{});
