@@ -189,7 +189,7 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
         ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
     e1.record(stream)
     e1.synchronize()
-    if int(out[0, 0].item()) != accepted:
+    if int(out[0, 0].item()) != accepted and os.environ.get("MVS_BENCH_WHATIF") != "1":
         raise RuntimeError(f"pack header {int(out[0, 0].item())} != {accepted} accepted")
     # the same pack without the points: 16-B rows [index, mask word]
     out16 = torch.empty((cap + 1, par.points_width(words, points=False)), dtype=torch.int64, device=sw["c"].device)
@@ -201,7 +201,7 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
         ctx.pack_accepted(sw["off"], pc, pm, vlb, out16, stream=stream.cuda_stream)
     e3.record(stream)
     e3.synchronize()
-    if int(out16[0, 0].item()) != accepted:
+    if int(out16[0, 0].item()) != accepted and os.environ.get("MVS_BENCH_WHATIF") != "1":
         raise RuntimeError(f"16-B pack header {int(out16[0, 0].item())} != {accepted} accepted")
     return {"row_bytes": row, "rows_per_rank": accepted, "bytes_per_rank": row * (cap + 1),
             "pack_us": e0.elapsed_time(e1) / 20 * 1e3,
@@ -522,7 +522,9 @@ def main():
         pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream)
         masked(False)
         del sw["exch"]
-        if packed != accepted:
+        # (MVS_BENCH_WHATIF=1: a measurement-only library built with
+        # MVS_TAB_WHATIF, whose wrong results vary from run to run)
+        if packed != accepted and os.environ.get("MVS_BENCH_WHATIF") != "1":
             raise RuntimeError(f"N = 1 pack: {packed} rows != {accepted} accepted")
         scaling_base = {"step_ms_with_pack": pdt / a.steps * 1e3, "value_with_pack": n * a.steps / pdt,
                         "step_ms_score_only": dt / a.steps * 1e3,

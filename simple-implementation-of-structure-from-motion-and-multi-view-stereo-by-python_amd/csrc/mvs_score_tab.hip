@@ -229,6 +229,9 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_TIXV
 #define MVS_TAB_TIXV 0
 #endif
+#ifndef MVS_TAB_STATIC_FIRST
+#define MVS_TAB_STATIC_FIRST 1
+#endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
@@ -341,6 +344,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         const int ty = d.x / t.ntx, tx = d.x - ty * t.ntx;
         const int x0 = tx * MVS_TILE_W, yr0 = ty * MVS_TILE_H - WID;
         uint8_t* base = region_buf(bufc);
+        if constexpr (!(MVS_TAB_WHATIF & 16))   // measurement only: no region DMA
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
             const int k = opaque(td) + p * DT;   // recomputed per piece: no long-lived offsets
@@ -393,7 +397,11 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         }
     };
 
-    auto claim = [&]() -> int { return atomicAdd(head, 1); };
+    // MVS_TAB_STATIC_FIRST: workgroup b's first two items are b and b + grid
+    // (no claim), the queue hands out the rest -- at the kernel's start the
+    // grid's 2 x 512 claims would otherwise queue on the one head counter
+    const int first = MVS_TAB_STATIC_FIRST ? 2 * (int)gridDim.x : 0;
+    auto claim = [&]() -> int { return atomicAdd(head, 1) + first; };
     // an item's descriptor (tile, first bucket entry, count, entries staged):
     // the list is staged as a whole chunk (bounded by the bucket), so that its
     // LDS-DMA needs no count -- the count arrives a round later
@@ -416,8 +424,8 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     // (DB) and its tile's count, item k+2's (tile, chunk) and thread 0's claim
     // of item k+3 are in flight
     if (tid == 0) {
-        s_ids[0] = claim();
-        s_ids[1] = claim();
+        s_ids[0] = MVS_TAB_STATIC_FIRST ? (int)blockIdx.x : claim();
+        s_ids[1] = MVS_TAB_STATIC_FIRST ? (int)(blockIdx.x + gridDim.x) : claim();
     }
     __syncthreads();
     int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
@@ -548,6 +556,9 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         if constexpr (LT) {
                             sa_raw[h] = ls_sb[tix + Rv[h]];
                             wa_raw[h] = w_of(ls_d[tix + Rv[h]]);
+                        } else if constexpr (MVS_TAB_WHATIF & 32) {   // measurement only: no S_a, w_a gathers
+                            sa_raw[h] = tix & 7;
+                            wa_raw[h] = 1.0;
                         } else {
                             sa_raw[h] = tsb[tix + Rv[h]];
                             wa_raw[h] = tw[tix + Rv[h]];
@@ -980,6 +991,8 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                             const double sum = self ? mine - inv : mine;
                             av = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
                         }
+                        if constexpr (MVS_TAB_WHATIF & 64) {   // measurement only: no output stores
+                        } else
                         if (a.rec) {
                             // one 16-B record [mask word, avg] (|V| = popcount)
                             const unsigned long long ab = __double_as_longlong(av);
