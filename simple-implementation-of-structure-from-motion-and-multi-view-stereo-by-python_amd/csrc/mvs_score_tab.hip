@@ -433,11 +433,15 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     if (cur >= n_units) return;
     int4 dcur;
     {
-        const int2 it = item_v(cur);
+        // an implicit item needs no load; the first DMA needs no count (its
+        // list is staged as a whole chunk), so it goes out before the count
+        const int2 it = implicit && cur < t.ntiles ? make_int2(cur, 0) : item_v(cur);
+        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y);
+        stage(make_int4(tile, tile * t.cap + j * t.chunk, 0, min(t.chunk, t.cap - j * t.chunk)),
+              std::integral_constant<int, 0>{});
         dcur = desc(it, count_v(it.x));
     }
-    stage(dcur, std::integral_constant<int, 0>{});
-    int2 it1 = nx1 < n_units ? item_v(nx1) : make_int2(0, 0);
+    int2 it1 = nx1 >= n_units ? make_int2(0, 0) : implicit && nx1 < t.ntiles ? make_int2(nx1, 0) : item_v(nx1);
     it1 = make_int2(__builtin_amdgcn_readfirstlane(it1.x), __builtin_amdgcn_readfirstlane(it1.y));
     int pend = 0;
     if (tid == 0) pend = claim();
