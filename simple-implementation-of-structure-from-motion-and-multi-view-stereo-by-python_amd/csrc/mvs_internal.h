@@ -219,6 +219,11 @@ struct ExpandArgs {
 #define MVS_MMA_CHUNK 1024    // candidates per work item, V <= 64 (whole tiles, as a rule)
 #define MVS_GROUP_VIEWS 64    // views per group when V > 64
 #define MVS_GROUP_CHUNK 116   // candidates per work item when V > 64 (their reference rows staged)
+// k_acc_pack A/B switch: every candidate's point loaded with its mask word
+// (1) or only the accepted ones' once the counts are in (0)
+#ifndef MVS_ACC_EAGER
+#define MVS_ACC_EAGER 0
+#endif
 #ifndef MVS_ACC_PER
 #define MVS_ACC_PER 8         // candidates per thread of the exchange's pack (A/B switch)
 #endif

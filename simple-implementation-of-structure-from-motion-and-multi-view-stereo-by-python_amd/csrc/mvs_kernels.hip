@@ -2258,11 +2258,27 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             }
         }
         double px[kAccPer], py[kAccPer], pz[kAccPer];
+#if MVS_ACC_EAGER
+        // every candidate's point in flight with its mask word (no round trip
+        // between the counts and the points; the rejected ones' are dropped)
+#pragma unroll
+        for (int j = 0; j < kAccPer; ++j) {
+            const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+            px[j] = py[j] = pz[j] = 0.0;
+            if (cpt && i < n) {
+                const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
+                px[j] = xy.x;
+                py[j] = xy.y;
+                pz[j] = cpt[3 * i + 2];
+            }
+        }
+#endif
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
             const bool acc = i < n && c[j] >= vlb;
             m[j] = __ballot(acc);
+#if !MVS_ACC_EAGER
             px[j] = py[j] = pz[j] = 0.0;
             if (cpt && acc) {
                 // x, y as one 16-B load (8-B aligned), z beside it
@@ -2271,6 +2287,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 py[j] = xy.y;
                 pz[j] = cpt[3 * i + 2];
             }
+#endif
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
         }
         lds_barrier();   // the points stay in flight

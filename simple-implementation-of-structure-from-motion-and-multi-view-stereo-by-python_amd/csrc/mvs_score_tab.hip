@@ -232,6 +232,22 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_STATIC_FIRST
 #define MVS_TAB_STATIC_FIRST 1
 #endif
+// MVS_TAB_TAIL_SPLIT: the last this-many tiles of a dense batch's implicit
+// items are queued as two half-items each (the first and the second half of
+// the tile's M-blocks; the region staged for both), so that the kernel's
+// last items -- which set its end -- are half as long
+#ifndef MVS_TAB_TAIL_SPLIT
+#define MVS_TAB_TAIL_SPLIT 0
+#endif
+// MVS_TAB_SHALLOW: a workgroup claims item k+2 while it scores item k (the
+// index goes round through LDS at the next round's barrier) instead of item
+// k+3 with item k+2's descriptor already loaded: one item fewer held back
+// when the queue runs dry, so the kernel's tail -- workgroups still working
+// off items they claimed early -- is one item shorter.  An implicit item's
+// descriptor is computed, not loaded, so nothing waits for it
+#ifndef MVS_TAB_SHALLOW
+#define MVS_TAB_SHALLOW 1
+#endif
 constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
 constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
@@ -307,6 +323,9 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     __shared__ __attribute__((aligned(16))) uint8_t s_tab0[LT ? TG::TS + TG::TD : 16], s_tab1[LT && DB ? TG::TS + TG::TD : 16];
     __shared__ int s_ids[2];
     __shared__ double s_recip[65];
+#ifdef MVS_STAMPS
+    const unsigned long long t_wg0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int V = sc.V;
@@ -326,7 +345,10 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     // implicit items: k < ntiles is (tile k, chunk 0), then segment 1's
     // further chunks (k_bin); else k_item_scan's list
     const bool implicit = t.implicit != 0;
-    const int n_units = implicit ? t.ntiles + t.n_items[32] : im.total();
+    // half-item code in bits 20+ of an item's chunk field: 0 whole, 1 / 2 = first / second half
+    const int tsplit = implicit ? min(MVS_TAB_TAIL_SPLIT, t.ntiles) : 0;
+    const int tsplit0 = t.ntiles - tsplit;
+    const int n_units = implicit ? t.ntiles + tsplit + t.n_items[32] : im.total();
     int32_t* head = t.head;
     const int16_t* __restrict__ tsb = mt.sb;
     const double* __restrict__ tw = mt.w;
@@ -406,7 +428,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     // the list is staged as a whole chunk (bounded by the bucket), so that its
     // LDS-DMA needs no count -- the count arrives a round later
     auto desc = [&](int2 it, int cnt) -> int4 {
-        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y);
+        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y & 0xfffff);
         const int c = __builtin_amdgcn_readfirstlane(cnt);
         return make_int4(tile, tile * t.cap + j * t.chunk, min(min(c, t.cap) - j * t.chunk, t.chunk),
                          min(t.chunk, t.cap - j * t.chunk));
@@ -416,8 +438,11 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     // read of the round
     auto item_v = [&](int v) -> int2 {
         // the load is issued either way (its wait stays the round end's vmcnt)
-        const int2 ld = *(const int2*)(items + opaque(implicit ? t.item_seg + max(v - t.ntiles, 0) : im.slot(v)));
-        return implicit && v < t.ntiles ? make_int2(v, 0) : ld;
+        const int2 ld = *(const int2*)(items + opaque(implicit ? t.item_seg + max(v - t.ntiles - tsplit, 0) : im.slot(v)));
+        if (implicit && v < tsplit0) return make_int2(v, 0);
+        if (implicit && v < t.ntiles + tsplit)
+            return make_int2(tsplit0 + ((v - tsplit0) >> 1), (1 + ((v - tsplit0) & 1)) << 20);
+        return ld;
     };
     auto count_v = [&](int tile) -> int { return t.tile_count[opaque(tile * kTcStride)]; };
     // the item pipeline: while item k is scored, item k+1's region and list
@@ -432,19 +457,26 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
     if (cur >= n_units) return;
     int4 dcur;
+    int hcur = 0;   // half-item code of the current item
     {
         // an implicit item needs no load; the first DMA needs no count (its
         // list is staged as a whole chunk), so it goes out before the count
-        const int2 it = implicit && cur < t.ntiles ? make_int2(cur, 0) : item_v(cur);
-        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y);
+        const int2 it = implicit && cur < tsplit0 ? make_int2(cur, 0) : item_v(cur);
+        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y & 0xfffff);
+        hcur = __builtin_amdgcn_readfirstlane(it.y >> 20);
         stage(make_int4(tile, tile * t.cap + j * t.chunk, 0, min(t.chunk, t.cap - j * t.chunk)),
               std::integral_constant<int, 0>{});
         dcur = desc(it, count_v(it.x));
     }
-    int2 it1 = nx1 >= n_units ? make_int2(0, 0) : implicit && nx1 < t.ntiles ? make_int2(nx1, 0) : item_v(nx1);
+#if MVS_TAB_SHALLOW
+    int2 it1 = make_int2(0, 0);
+    int pend = nx1;   // thread 0's: the next item, published at round 0's barrier
+#else
+    int2 it1 = nx1 >= n_units ? make_int2(0, 0) : implicit && nx1 < tsplit0 ? make_int2(nx1, 0) : item_v(nx1);
     it1 = make_int2(__builtin_amdgcn_readfirstlane(it1.x), __builtin_amdgcn_readfirstlane(it1.y));
     int pend = 0;
     if (tid == 0) pend = claim();
+#endif
     __syncthreads();   // everyone has read s_ids before they are rewritten
 
     auto round = [&](auto bufc) -> bool {
@@ -461,26 +493,45 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's LDS-DMA, before the barrier
         __syncthreads();
         TSTAMP(ts1);
+#if MVS_TAB_SHALLOW
+        // item k+1 (claimed last round), its region and list into the other
+        // buffer and its count; thread 0's claim of item k+2
+        nx1 = __builtin_amdgcn_readfirstlane(s_ids[0]);
+        if (nx1 < n_units) {
+            const int2 iv = item_v(nx1);   // implicit: computed; else a load waited for here
+            it1 = make_int2(__builtin_amdgcn_readfirstlane(iv.x), __builtin_amdgcn_readfirstlane(iv.y));
+        }
+#else
         const int nx2 = __builtin_amdgcn_readfirstlane(s_ids[0]);
         // item k+2's (tile, chunk) and item k+1's count (consumed at the
         // round's end), item k+1's region and list into the other buffer,
         // thread 0's claim of the one after that
-        const int4 dst1 = make_int4(it1.x, it1.x * t.cap + it1.y * t.chunk, 0, min(t.chunk, t.cap - it1.y * t.chunk));
+#endif
+        const int j1 = it1.y & 0xfffff;
+        const int4 dst1 = make_int4(it1.x, it1.x * t.cap + j1 * t.chunk, 0, min(t.chunk, t.cap - j1 * t.chunk));
         if constexpr (DB && !MVS_TAB_DMA_LATE) {
             if (nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
         }
+#if MVS_TAB_SHALLOW
+        const int c1 = count_v(it1.x);
+        if (nx1 < n_units && tid == 0) pend = claim();
+#else
         // unconditional (clamped) loads: no branch, no register reset that
         // would wait for the LDS-DMA just issued
         const int2 it2 = item_v(min(nx2, n_units - 1));
         const int c1 = count_v(it1.x);
         if (nx2 < n_units && tid == 0) pend = claim();
+#endif
         TSTAMP(ts1b);
         TSTAMP_ADD(7, ts1b - ts1);
         const int ty = dcur.x / t.ntx, tx = dcur.x - ty * t.ntx;
         const int tix0 = ((ty * MVS_TILE_H) * sc.W + tx * MVS_TILE_W) * VP;   // table element of the tile origin
         // ---- 2. this wave's M-blocks, sorted by row pair inside the wave ----
-        const int nblk = (nc + 15) >> 4;
-        const int b0 = (nblk * wave) >> 3, b1 = (nblk * (wave + 1)) >> 3;
+        const int nblk_all = (nc + 15) >> 4;
+        // a half-item: its half of the M-blocks
+        const int blo = hcur == 2 ? nblk_all >> 1 : 0, bhi = hcur == 1 ? nblk_all >> 1 : nblk_all;
+        const int nblk = bhi - blo;
+        const int b0 = blo + ((nblk * wave) >> 3), b1 = blo + ((nblk * (wave + 1)) >> 3);
         {
             const int base = 16 * b0, cnt = min(16 * b1, nc) - base;   // <= 128
             // one stable counting pass by the digit (pk >> SH) & (NBINS - 1)
@@ -1037,14 +1088,29 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         }
         cur = nx1;
         dcur = desc(it1, c1);
+        hcur = __builtin_amdgcn_readfirstlane(it1.y >> 20);
+#if !MVS_TAB_SHALLOW
         nx1 = nx2;
         it1 = make_int2(__builtin_amdgcn_readfirstlane(it2.x), __builtin_amdgcn_readfirstlane(it2.y));
+#endif
         return true;
     };
     for (;;) {
         if (!round(std::integral_constant<int, 0>{})) break;
         if (!round(std::integral_constant<int, DB ? 1 : 0>{})) break;
     }
+#ifdef MVS_STAMPS
+    // the workgroup's start and end on the 100 MHz clock (slots 10, 11; thread 0)
+    if (tid == 0) {
+        atomicAdd(&g_stamps_tab[(blockIdx.x & 1023) * 16 + 10], (unsigned long long)t_wg0);
+        atomicAdd(&g_stamps_tab[(blockIdx.x & 1023) * 16 + 11], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        // where it ran: HW_ID (CU, SH, SE) and XCC_ID, + 1 (slots 12, 13)
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
+        atomicAdd(&g_stamps_tab[(blockIdx.x & 1023) * 16 + 12], (unsigned long long)hw + 1ull);
+        atomicAdd(&g_stamps_tab[(blockIdx.x & 1023) * 16 + 13], (unsigned long long)xcc + 1ull);
+    }
+#endif
 }
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is not needed: all LDS is static
