@@ -154,6 +154,12 @@ struct TiledArgs {
 // 27.7-28.0 (profiles/r05/r5m_ab_bin3.log): the scatter alone, now a kernel
 // of its own, costs 15 us -- the bucket writes land as partial lines from
 // every XCD -- where k_bin hides it behind its own chain
+// k_bin A/B switch: two neighbouring tiles' counters per 64-bit returning
+// atomic (~40 % fewer atomics).  Measured slower: 34.3-34.5 vs 27.7-27.9 us
+// (profiles/r05/r5bp_ab_bin_pairs.log)
+#ifndef MVS_BIN_PAIRS
+#define MVS_BIN_PAIRS 0
+#endif
 #ifndef MVS_BIN3
 #define MVS_BIN3 0
 #endif
