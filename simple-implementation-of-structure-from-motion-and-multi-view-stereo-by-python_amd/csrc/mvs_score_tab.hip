@@ -194,7 +194,7 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 // that issue none never wait for the next item's region at their table
 // gathers; the issuing waves take the DMA's instruction cost
 #ifndef MVS_TAB_DMA_WAVES
-#define MVS_TAB_DMA_WAVES 8
+#define MVS_TAB_DMA_WAVES 64   // all of the workgroup's waves
 #endif
 // MVS_TAB_DMA_LATE (A/B switch): a wave issues its part of the next item's
 // LDS-DMA after its first unit instead of at the round's start, so that its
@@ -255,9 +255,14 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_LATE_CLAIM
 #define MVS_TAB_LATE_CLAIM 1
 #endif
-constexpr int kTabThreads = 512, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
+// MVS_TAB_WAVES (A/B switch): waves per workgroup (two workgroups per CU).
+// 10 (5 per SIMD, 96 VGPRs with spills): 134.6-135.4 vs 88.4 us (r5wv_*)
+#ifndef MVS_TAB_WAVES
+#define MVS_TAB_WAVES 8
+#endif
+constexpr int kTabThreads = 64 * MVS_TAB_WAVES, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
 constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
-constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : 4;                                // per SIMD
+constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : (2 * kTabWaves + 3) / 4;            // per SIMD
 constexpr int kTabChunk = MVS_MMA_CHUNK;
 
 // a candidate's constants in a unit (per wave, 32 slots)
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     constexpr bool DB = TG::DB, LT = TG::LT;
 
     constexpr int RPV = VS / 32;                                          // region rows per view incl. the pad row
-    constexpr int DW = MVS_TAB_DMA_WAVES, DT = DW * 64;                   // the DMA's waves and threads
+    constexpr int DW = MVS_TAB_DMA_WAVES < kTabWaves ? MVS_TAB_DMA_WAVES : kTabWaves, DT = DW * 64;   // the DMA's waves and threads
     static_assert(DW >= 1 && DW <= kTabWaves, "DMA waves");
     constexpr int PF = (VP * RPV * 2 + DT - 1) / DT;                      // 16-B pieces per DMA thread
     constexpr int RB = TG::RB, CB = TG::CB;
@@ -538,7 +543,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         // a half-item: its half of the M-blocks
         const int blo = hcur == 2 ? nblk_all >> 1 : 0, bhi = hcur == 1 ? nblk_all >> 1 : nblk_all;
         const int nblk = bhi - blo;
-        const int b0 = blo + ((nblk * wave) >> 3), b1 = blo + ((nblk * (wave + 1)) >> 3);
+        const int b0 = blo + nblk * wave / kTabWaves, b1 = blo + nblk * (wave + 1) / kTabWaves;
         {
             const int base = 16 * b0, cnt = min(16 * b1, nc) - base;   // <= 128
             // one stable counting pass by the digit (pk >> SH) & (NBINS - 1)
