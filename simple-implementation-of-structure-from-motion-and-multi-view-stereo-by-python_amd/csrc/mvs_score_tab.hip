@@ -229,6 +229,9 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #ifndef MVS_TAB_TIXV
 #define MVS_TAB_TIXV 0
 #endif
+#ifndef MVS_TAB_NOPAD
+#define MVS_TAB_NOPAD 1
+#endif
 #ifndef MVS_TAB_STATIC_FIRST
 #define MVS_TAB_STATIC_FIRST 1
 #endif
@@ -382,8 +385,9 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
             const int k = opaque(td) + p * DT;   // recomputed per piece: no long-lived offsets
-            if (k < npiece) {
-                const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
+            const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
+            // MVS_TAB_NOPAD: the pad row (never read) is not loaded (its lanes masked)
+            if (k < npiece && (!MVS_TAB_NOPAD || (r2 >> 1) != RPV - 1)) {
                 const int y = min(max(yr0 + (r2 >> 1), 0), sc.H - 1);
                 const uint8_t* src = sc.gv + ((int64_t)v * sc.H + y) * sc.Wp + (x0 - 8) + 16 * (r2 & 1);
                 __builtin_amdgcn_global_load_lds((const void*)src,
