@@ -58,7 +58,10 @@ PEAK_HBM = 8.0e12          # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
 PEAK_I8 = 5.0e15           # dense i8 MFMA ops/s (2x the 2.5 PF dense bf16; no sparsity)
 SIMDS = 1024               # 256 CUs x 4 SIMDs
 CLOCK = 2.4e9              # peak engine clock, Hz
-PMC_PATH = os.path.join(REPO, "profiles", "r05", "pmc.json")
+# per-launch PMC counters of the scorers (tools/pmc.sh + tools/pmc_json.py):
+# this round's profile, else the last round's
+PMC_PATH = next((p for p in (os.path.join(REPO, "profiles", r, "pmc.json") for r in ("r06", "r05"))
+                 if os.path.exists(p)), os.path.join(REPO, "profiles", "r06", "pmc.json"))
 # kernel / score-call timing: HIP and torch events on every TIME_EVERY-th timed
 # step (the records cost the stream a few us each: sampled, not every step)
 TIME_EVERY = 10
@@ -67,6 +70,21 @@ TIME_EVERY = 10
 def logical_bytes(V, wid):
     """V*(2w+1)^2 window bytes + 32 B in + 8*ceil(V/64) + 16 B out."""
     return V * (2 * wid + 1) ** 2 + 32 + 8 * ((V + 63) // 64) + 16
+
+
+def floor_bytes(V, H, W, n):
+    """The unique bytes one scorer launch must move between HBM and the
+    chip: the scene's moment tables (S_b int16 + w binary64 per (pixel,
+    view) at V <= 64, S_b int16 + D int32 at V > 64; (H W + 16) VP entries),
+    the view-major gray copy gv (V H Wp bytes, Wp = 16-aligned W + 32), the
+    bucket entries read (8 B per candidate) and the records written
+    (8 (ceil(V/64) + 1) B per candidate)."""
+    words = (V + 63) // 64
+    vp = 64 * words if V > 64 else 16 * ((V + 15) // 16)
+    tables = (H * W + 16) * vp * (6 if V > 64 else 10)
+    wp = (W + 15) // 16 * 16 + 32
+    parts = {"tables": tables, "gv": V * H * wp, "bucket_entries": 8 * n, "records": 8 * (words + 1) * n}
+    return sum(parts.values()), parts
 
 
 def score(cx, sw, wid, thr, stream, rec=None):
@@ -126,17 +144,47 @@ def pmc_entry(scene, V, wid, n, kernel):
     return None
 
 
-def roofline(entry, V, wid, n, kms, kernel):
+def scorer_stats(ctx):
+    """MvsContext.scorer_stats(), or zeros from an older A/B library (MVS_LIB)
+    without the entry point."""
+    try:
+        st = ctx.scorer_stats()
+    except AttributeError:
+        st = {"direct": 0, "overflow": 0, "batches": 0}
+    st["exact"] = ctx.exact_hits()
+    return st
+
+
+def direct_path(before, after):
+    """Candidates per sweep that k_score_fix re-scored by the direct path
+    (the tiled scorer's binary32 guard band + bucket overflow), from two
+    MvsContext.scorer_stats() readings."""
+    b = max(after["batches"] - before["batches"], 1)
+    d = after["direct"] - before["direct"]
+    o = after["overflow"] - before["overflow"]
+    return {"per_sweep": d / b, "overflow_per_sweep": o / b, "guard_band_per_sweep": (d - o) / b,
+            "numpy_order_ncc_per_sweep": (after["exact"] - before["exact"]) / b, "sweeps": b}
+
+
+def roofline(entry, V, H, W, wid, n, kms, kernel):
     """Roofs of the dominant kernel: measured HBM bytes, VALU-busy cycles and
     MFMA i8 operations per launch (PMC) over the live launch time.  The binding
     roof is the one with the largest fraction; each frac <= 1 because a unit
-    cannot be busier than its peak."""
+    cannot be busier than its peak.  Beside them the unique-byte floor of a
+    launch (floor_bytes): useful_frac = floor / launch time / 8 TB/s, and
+    traffic / floor = how much of the counted traffic is re-reads."""
     npx = (2 * wid + 1) ** 2
+    fb, fparts = floor_bytes(V, H, W, n)
     out = {"kernel": entry["kernel"] if entry else kernel, "kernel_ms": kms,
-           "candidates_per_launch": n, "logical_bytes_per_candidate": logical_bytes(V, wid),
-           "logical_GBps": logical_bytes(V, wid) * n / (kms * 1e-3) / 1e9,
-           "logical_note": "SURVEY 8(d) bytes (every candidate's V windows read once); the scorer "
-                           "stages each tile's region once, so this is not a traffic figure"}
+           "candidates_per_launch": n,
+           "floor_bytes": fb, "floor_parts": fparts,
+           "useful_GBps": fb / (kms * 1e-3) / 1e9,
+           "useful_frac": fb / (kms * 1e-3) / PEAK_HBM,
+           "survey_model_bytes_per_candidate": logical_bytes(V, wid),
+           "survey_model_note": "SURVEY 8(d) prices a candidate at V (2w+1)^2 + 56 B (every window read "
+                                "once per candidate); the scorer stages a tile's region once for all "
+                                "its candidates, so that model exceeds the HBM peak by construction "
+                                "and is no traffic figure: floor_bytes is"}
     roofs = {}
     useful = 2.0 * V * npx * n        # the window products sum s_R s_v of all V views
     roofs["mfma_useful"] = {"achieved": useful / (kms * 1e-3) / 1e12, "peak": PEAK_I8 / 1e12,
@@ -146,7 +194,10 @@ def roofline(entry, V, wid, n, kms, kernel):
         c = entry["per_launch"]
         traffic = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
         roofs["hbm"] = {"achieved": traffic / (kms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                        "bytes_per_launch": traffic}
+                        "bytes_per_launch": traffic,
+                        "note": "2 x FETCH_SIZE + WRITE_SIZE: FETCH counts Infinity-Cache (MALL) hits too, "
+                                "so on a cache-resident scene this is L2-miss traffic, not DRAM bytes"}
+        out["traffic_over_floor"] = traffic / fb
         valu = c["SQ_ACTIVE_INST_VALU"] * 4.0            # quad-cycles -> cycles, summed over SIMDs
         roofs["valu"] = {"achieved": valu / (kms * 1e-3) / 1e9, "peak": SIMDS * CLOCK / 1e9,
                          "unit": "G SIMD-busy-cycles/s",
@@ -189,7 +240,7 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
         ctx.pack_accepted(sw["off"], pc, pm, vlb, out, stream=stream.cuda_stream, c=sw["c"])
     e1.record(stream)
     e1.synchronize()
-    if int(out[0, 0].item()) != accepted and os.environ.get("MVS_BENCH_WHATIF") != "1":
+    if int(out[0, 0].item()) != accepted:
         raise RuntimeError(f"pack header {int(out[0, 0].item())} != {accepted} accepted")
     # the same pack without the points: 16-B rows [index, mask word]
     out16 = torch.empty((cap + 1, par.points_width(words, points=False)), dtype=torch.int64, device=sw["c"].device)
@@ -201,7 +252,7 @@ def exchange_figures(ctx, sw, V, vlb, accepted, world, stream, thr, wid):
         ctx.pack_accepted(sw["off"], pc, pm, vlb, out16, stream=stream.cuda_stream)
     e3.record(stream)
     e3.synchronize()
-    if int(out16[0, 0].item()) != accepted and os.environ.get("MVS_BENCH_WHATIF") != "1":
+    if int(out16[0, 0].item()) != accepted:
         raise RuntimeError(f"16-B pack header {int(out16[0, 0].item())} != {accepted} accepted")
     return {"row_bytes": row, "rows_per_rank": accepted, "bytes_per_rank": row * (cap + 1),
             "pack_us": e0.elapsed_time(e1) / 20 * 1e3,
@@ -336,6 +387,10 @@ def main():
     a = ap.parse_args(argv)
     if a.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
+    if a.pack_on_comm and a.soa:
+        # the SoA outputs are single-buffered: the next sweep would overwrite
+        # count / mask while the comm stream's pack still reads them
+        raise SystemExit("--pack-on-comm needs the record outputs (not --soa)")
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # no launcher: this process starts the ranks and never touches the GPU
         sys.exit(launch_ranks(a.gpus))
@@ -476,11 +531,15 @@ def main():
     # (all CUs but --comm-cus), the scorer's grid at two workgroups per kept
     # CU, and the pack + all-gather on the exchange's stream, where they find
     # the free CUs instead of queueing behind the persistent scorer
-    mstream, kept, cstream = stream, None, None
+    mstream, kept, cstream, cowner, owners = stream, None, None, None, []
     if a.comm_cus > 0 and (world > 1 or rank == 0):
         if a.comm_layout == "mask":
-            mstream, kept = par.cu_masked_stream(dev, a.comm_cus)
-            cstream, _ = par.cu_masked_stream(dev, a.comm_cus, complement=True)
+            # the streams' owners (parallel.MaskedStream): closed at the end,
+            # or at exit by their atexit hook
+            mowner = par.cu_masked_stream(dev, a.comm_cus)
+            cowner = par.cu_masked_stream(dev, a.comm_cus, complement=True)
+            owners = [mowner, cowner]
+            mstream, kept, cstream = mowner.stream, mowner.cus, cowner.stream
         else:
             kept = torch.cuda.get_device_properties(dev).multi_processor_count - a.comm_cus
 
@@ -497,10 +556,12 @@ def main():
         dist.all_reduce(kk, op=dist.ReduceOp.MAX)
         cap = int(kk.item()) + int(kk.item()) // 16 + 256
         sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap, dev, pack_on_comm=pack_on_comm,
-                                        comm_stream=cstream if pack_on_comm else None)
+                                        comm_stream=cowner if pack_on_comm else None)
         masked(True)
     total_n = a.n if a.strong else a.n * world
+    st0 = scorer_stats(ctx)
     dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream if world > 1 else stream)
+    direct = direct_path(st0, scorer_stats(ctx))
     masked(False)
     value = total_n * a.steps / dt
     accepted = int((host_outputs(sw)[1] >= vlb).sum())
@@ -517,14 +578,12 @@ def main():
         # 1 -> N comparison can also be made on the same device work
         cap1 = accepted + accepted // 16 + 256
         sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap1, dev, pack_on_comm=pack_on_comm,
-                                        comm_stream=cstream if pack_on_comm else None)
+                                        comm_stream=cowner if pack_on_comm else None)
         masked(True)
         pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream)
         masked(False)
         del sw["exch"]
-        # (MVS_BENCH_WHATIF=1: a measurement-only library built with
-        # MVS_TAB_WHATIF, whose wrong results vary from run to run)
-        if packed != accepted and os.environ.get("MVS_BENCH_WHATIF") != "1":
+        if packed != accepted:
             raise RuntimeError(f"N = 1 pack: {packed} rows != {accepted} accepted")
         scaling_base = {"step_ms_with_pack": pdt / a.steps * 1e3, "value_with_pack": n * a.steps / pdt,
                         "step_ms_score_only": dt / a.steps * 1e3,
@@ -577,9 +636,10 @@ def main():
         "score_call_ms": pms,
         "accepted_per_sweep": accepted,
         "gathered_records": gathered,
+        "direct_path": direct,
         "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream, a.thr, a.wid),
     }
-    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms, kernel_name)
+    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, H, W, a.wid, n, kms, kernel_name)
     if solo and not a.no_overlap:
         # the multi-GPU layout: scoring on the CU-masked stream, the pack and
         # the proxy of RCCL's all-gather on the CUs it leaves out
@@ -609,11 +669,12 @@ def main():
                                      "before every sweep; the warm figure is `value`"}
         if a.secondary_wid and a.secondary_wid != a.wid:
             s2 = max(a.steps // 2, 5)
+            st0 = scorer_stats(ctx)
             dt2, kms2, pms2, _ = timed(ctx, sw, a.secondary_wid, s2, 2, exchange=False)
             out["secondary"] = {"wid": a.secondary_wid, "value": n * s2 / dt2, "kernel_ms": kms2,
-                                "score_call_ms": pms2,
+                                "score_call_ms": pms2, "direct_path": direct_path(st0, scorer_stats(ctx)),
                                 "roofline": roofline(pmc_entry(a.scene, V, a.secondary_wid, n, kernel_name), V,
-                                                     a.secondary_wid, n, kms2, kernel_name)}
+                                                     H, W, a.secondary_wid, n, kms2, kernel_name)}
 
     if solo and a.scene == "dino" and not a.no_stage:
         sd = dict(np.load(os.path.join(REPO, "tests", "golden", "seeds_dino.npz")))
@@ -650,8 +711,8 @@ def main():
                           "value": rsw["n"] * s3 / rdt, "unit": "candidates/s", "kernel": rctx.timed_kernel(),
                           "kernel_ms": rkms, "score_call_ms": rpms,
                           "accepted_per_sweep": int((host_outputs(rsw)[1] >= 3).sum()),
-                          "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"], rctx.timed_kernel()), rV, a.wid,
-                                               rsw["n"], rkms, rctx.timed_kernel())}
+                          "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"], rctx.timed_kernel()), rV, rH,
+                                               rW, a.wid, rsw["n"], rkms, rctx.timed_kernel())}
         rctx.close()
 
     if solo and not a.no_cpu_baseline:
@@ -696,9 +757,8 @@ def main():
     if rank == 0:
         print(json.dumps(out))
     sw.pop("exch", None)
-    for s_ in (mstream, cstream):
-        if s_ is not None and s_ is not stream:
-            par.destroy_stream(s_)
+    for o in owners:
+        o.close()
     if world > 1:
         dist.destroy_process_group()
     ctx.close()

@@ -162,6 +162,24 @@ const char* mvs_timed_kernel(const mvs_ctx* ctx);
  * context was created.  (The tiled scorer's own band, 2e-6 relative on its
  * binary32 comparison, sends a candidate to the direct scorer.) */
 int64_t mvs_exact_hits(mvs_ctx* ctx);
+/* A caller stream that a *_device call has used is about to be destroyed
+ * (hipStreamDestroy): the context waits for that stream's work on its
+ * scratch and pack areas now.  The context orders calls made on different
+ * streams by an event recorded lazily on the stream that used an area last,
+ * when the next call comes from another stream; a destroyed stream cannot
+ * take that record (its handle may even be reused by a new stream), so a
+ * caller that retires streams calls this first, on every context the stream
+ * has used (parallel.MaskedStream.close does).  Streams the caller keeps
+ * need nothing. */
+int mvs_stream_retiring(mvs_ctx* ctx, void* stream);
+
+/* Direct-path statistics of the tiled scorers since the context was created
+ * (device work ordered before this call on the context's stream is counted;
+ * call after synchronising the streams that scored): out[0] = candidates
+ * re-scored by the direct path (k_score_fix: the tiled scorer's guard band
+ * plus bucket overflow), out[1] = of them bucket overflow, out[2] = tiled
+ * batches.  Diagnostic (bench.py reports the guard-band rate per sweep). */
+int mvs_scorer_stats(mvs_ctx* ctx, int64_t* out);
 
 /* ctNcc (MVS2.py:39-43) on n explicit window pairs of npx (<= 128) uint8
  * pixels each (device pointers).  ncc[i] = closed-form value (numpy-order

@@ -4,8 +4,10 @@ The product path has no CPU fallback: if the HIP library is missing or fails
 to load, every entry point raises RuntimeError (the one exception the
 reference's main() catches, main.py:43-46).
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -44,6 +46,8 @@ SIGNATURES = [
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
                                            _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
     ("mvs_exact_hits", ctypes.c_int64, [_vp]),
+    ("mvs_scorer_stats", ctypes.c_int, [_vp, _i64p]),
+    ("mvs_stream_retiring", ctypes.c_int, [_vp, _vp]),
     ("mvs_kernel_timing", ctypes.c_int, [_vp, ctypes.c_int]),
     ("mvs_kernel_time", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_int64)]),
@@ -108,6 +112,8 @@ def load(path=None):
     except OSError as e:
         raise RuntimeError(f"cannot load {path}: {e}") from e
     for name, res, args in SIGNATURES:
+        if path != LIB_PATH and not hasattr(lib, name):
+            continue   # an older A/B build (MVS_LIB) without a newer entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -195,6 +201,30 @@ def triangulate(P1, P2, x1, x2):
     return out
 
 
+# live contexts: a retiring caller stream is announced to each of them
+# (stream_retiring), and the ones still open at interpreter exit are closed by
+# an atexit hook, before the HIP runtime's own teardown
+_LIVE = weakref.WeakSet()
+
+
+def stream_retiring(stream):
+    """A caller stream (a hipStream_t handle) is about to be destroyed: every
+    live context waits for its work there now (mvs_stream_retiring)."""
+    for cx in list(_LIVE):
+        h = getattr(cx, "_h", None)
+        if h:
+            check(load().mvs_stream_retiring(h, stream), h, "mvs_stream_retiring")
+
+
+@atexit.register
+def _close_live_contexts():
+    for cx in list(_LIVE):
+        try:
+            cx.close()
+        except Exception:
+            pass
+
+
 class MvsContext:
     """One device-resident scene (images + cameras) on one GPU.
 
@@ -220,9 +250,14 @@ class MvsContext:
         check(rc, None, "mvs_ctx_create")
         self._h = h
         self.device = device
+        self._stages = weakref.WeakSet()
+        _LIVE.add(self)
 
     def close(self):
         if getattr(self, "_h", None):
+            # stepped stages hold the context: they go first
+            for st in list(getattr(self, "_stages", ())):
+                st.close()
             load().mvs_ctx_destroy(self._h)
             self._h = None
 
@@ -249,6 +284,14 @@ class MvsContext:
 
     def exact_hits(self):
         return int(load().mvs_exact_hits(self._h))
+
+    def scorer_stats(self):
+        """{'direct': candidates the direct path re-scored (guard band +
+        bucket overflow), 'overflow': of them bucket overflow, 'batches':
+        tiled batches} since the context was created (mvs_scorer_stats)."""
+        out = np.zeros(3, np.int64)
+        check(load().mvs_scorer_stats(self._h, _p(out, _i64p)), self._h, "mvs_scorer_stats")
+        return {"direct": int(out[0]), "overflow": int(out[1]), "batches": int(out[2])}
 
     def rebuild(self, stream=None):
         """Rebuild the device gray stack / view-major copy from the resident
@@ -506,6 +549,7 @@ class Stage:
         check(rc, ctx.handle, "mvs_stage_begin")
         self._st = h
         self.width = lib.mvs_stage_record_width(h)
+        ctx._stages.add(self)   # closed before their context (MvsContext.close)
 
     def plan(self):
         """Commit and plan the next sweep -> its job count (0: finished)."""

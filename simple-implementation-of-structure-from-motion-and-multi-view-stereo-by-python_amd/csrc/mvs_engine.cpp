@@ -300,6 +300,7 @@ struct mvs_ctx {
     DevBuf<uint8_t> d_rgb, d_stack, d_gv;
     DevBuf<CamDev> d_cams;
     DevBuf<int32_t> d_exact;
+    DevBuf<unsigned long long> d_stats;   // mvs_scorer_stats (k_score_fix)
     SceneDev sc{};
     // scratch for host-pointer scoring
     DevBuf<double> s_c, s_xy, s_avg;
@@ -307,7 +308,6 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand;
-    DevBuf<int32_t> t_bin;   // MVS_BIN3: binning workgroups' tile histograms + per-candidate words
     // mvs_pack_accepted: the chunks' look-back words (one per MVS_ACC_CHUNK
     // candidates), their epoch and the give-up counter
     DevBuf<uint64_t> p_status;
@@ -328,28 +328,26 @@ struct mvs_ctx {
     int tab_mode = 0;
     int scorer_wgs = 0;   // env MVS_SCORER_WGS: k_score_tab's grid (0 = every CU, twice)
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
-    DevBuf<double> mom_w[MVS_MAX_WID + 1];     // 48 < V <= 64
-    DevBuf<float> mom_wf[MVS_MAX_WID + 1];     // with mom_w: (float)w
-    DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V <= 48 or V > 64 (moments_dtab)
+    DevBuf<double> mom_w[MVS_MAX_WID + 1];     // V <= 64
+    DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V > 64 (moments_dtab)
     bool mom_ok[MVS_MAX_WID + 1] = {};
     int moments_vp() const { return V > MVS_GROUP_VIEWS ? 64 * ((V + 63) / 64) : 16 * ((V + 15) / 16); }
     MomentsDev moments(int wid) const {
         MomentsDev m{};
         m.sb = mom_sb[wid].p;
         m.w = mom_w[wid].p;
-        m.wf = mom_wf[wid].p;
         m.d = mom_d[wid].p;
         m.VP = moments_vp();
         m.wid = wid;
         return m;
     }
     // the tables of wid (10 B per (pixel, view) at V <= 64: S_b and w; 6 B at
-    // V > 64 or V <= MVS_TAB_LT_VIEWS: S_b and D), built on stream s if needed; false when they do not
+    // V > 64: S_b and D), built on stream s if needed; false when they do not
     // apply (disabled, or more than 2^31 elements).  One row of 16 pixels
     // past the end: k_score_tab stages a tile's rows whole (16 pixels x VP),
     // also where the last tile column runs past W
     // Memory: (H W + 16) VP elements per wid, 10 B each at V <= 64 (S_b int16
-    // + w binary64; + 4 B of binary32 w with MVS_TAB_SPLIT) or 6 B at V > 64
+    // + w binary64) or 6 B at V > 64
     // (S_b + D int32): 147 MB per wid at dinoRing, 3.2 GB at 256 x 1920 x 1080.  A scene past tab_limit elements (2^31;
     // env MVS_TAB_LIMIT lowers it, for tests) or whose tables cannot be
     // allocated is scored with the in-kernel moments instead (same results).
@@ -362,25 +360,19 @@ struct mvs_ctx {
             try {
                 mom_sb[wid].alloc((size_t)elems);
                 if (moments_dtab(V)) mom_d[wid].alloc((size_t)elems);
-                else {
-                    mom_w[wid].alloc((size_t)elems);
-                    if (MVS_TAB_SPLIT) mom_wf[wid].alloc((size_t)elems);
-                }
+                else mom_w[wid].alloc((size_t)elems);
             } catch (const Fail&) {
                 mom_sb[wid].release();
                 mom_d[wid].release();
                 mom_w[wid].release();
-                mom_wf[wid].release();
                 (void)hipGetLastError();   // the failed hipMalloc's error is not this call's
                 return false;
             }
             HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
             if (moments_dtab(V))
                 HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
-            else {
+            else
                 HIPCHK(hipMemsetAsync(mom_w[wid].p, 0, (size_t)elems * sizeof(double), s));
-                if (mom_wf[wid].p) HIPCHK(hipMemsetAsync(mom_wf[wid].p, 0, (size_t)elems * sizeof(float), s));
-            }
             const MomentsDev m = moments(wid);
             if (mvs_launch_moments(&sc, &m, s) != 0) throw Fail{MVS_E_HIP, "moments launch failed"};
             mom_ok[wid] = true;
@@ -423,6 +415,14 @@ struct mvs_ctx {
         void release(hipStream_t cur) {
             s = cur;
             used = true;
+        }
+        // the stream st is about to be destroyed: its work on the area is
+        // waited for now, so no later acquire records an event on it
+        void retire(hipStream_t st) {
+            if (!used || s != st) return;
+            HIPCHK(hipStreamSynchronize(st));
+            used = false;
+            s = nullptr;
         }
     } scratch_order, pack_order;
     std::string err;
@@ -577,17 +577,9 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.item_seg = (int)(n / std::max(t.chunk, 1) + ntiles + 2);
         ctx->t_items.ensure((size_t)kItemSegs * t.item_seg);
         t.items = ctx->t_items.p;
-        if (MVS_BIN3 && ntiles <= 16384) {
-            // one histogram row per binning workgroup, then an int2 per candidate
-            const int64_t nbin = (n + MVS_BIN_CHUNK - 1) / MVS_BIN_CHUNK;
-            const int64_t rows = (nbin * ntiles + 1) & ~(int64_t)1;
-            ctx->t_bin.ensure((size_t)(rows + 2 * n));
-            t.bin_rows = ctx->t_bin.p;
-            t.bin_scratch = (int2*)(ctx->t_bin.p + rows);
-            t.bin_words = rows + 2 * n;
-        }
         t.zero_first = ctx->tiles_clean_ntiles != ntiles ? 1 : 0;
         t.grid = ctx->scorer_wgs;
+        t.stats = ctx->d_stats.p;
         ctx->tiles_clean_ntiles = -1;            // dirty until the sequence is queued
         hipEvent_t e0, e1;
         ctx->next_events(&e0, &e1);
@@ -1413,6 +1405,8 @@ int mvs_ctx_create(int device, int V, int H, int W, const uint8_t* rgb, const do
         HIPCHK(hipMemcpyAsync(ctx->d_cams.p, ctx->cams.data(), V * sizeof(CamDev), hipMemcpyHostToDevice, ctx->stream));
         ctx->d_exact.alloc(1);
         HIPCHK(hipMemsetAsync(ctx->d_exact.p, 0, sizeof(int32_t), ctx->stream));
+        ctx->d_stats.alloc(4);
+        HIPCHK(hipMemsetAsync(ctx->d_stats.p, 0, 4 * sizeof(unsigned long long), ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
         ctx->sc.cams = ctx->d_cams.p;
         if (const char* km = std::getenv("MVS_SCORE_KERNEL")) {
@@ -1636,6 +1630,27 @@ int64_t mvs_exact_hits(mvs_ctx* ctx) {
         return 0;
     });
     return rc ? rc : h;
+}
+
+int mvs_stream_retiring(mvs_ctx* ctx, void* stream) {
+    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
+    if (!stream) return 0;   // the library's own stream is never retired by a caller
+    return guarded(ctx, [&]() {
+        ctx->scratch_order.retire((hipStream_t)stream);
+        ctx->pack_order.retire((hipStream_t)stream);
+        return 0;
+    });
+}
+
+int mvs_scorer_stats(mvs_ctx* ctx, int64_t* out) {
+    if (!ctx || !out) return set_err(ctx, Fail{MVS_E_ARG, "null argument"});
+    return guarded(ctx, [&]() {
+        unsigned long long h[4] = {0, 0, 0, 0};
+        HIPCHK(hipMemcpyAsync(h, ctx->d_stats.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        for (int k = 0; k < 3; ++k) out[k] = (int64_t)h[k];
+        return 0;
+    });
 }
 
 int mvs_ncc_windows(int64_t n, int npx, const uint8_t* d_a, const uint8_t* d_b, double thr,

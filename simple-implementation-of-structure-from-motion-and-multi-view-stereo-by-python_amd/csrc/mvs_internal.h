@@ -84,23 +84,9 @@ constexpr int kItemSegs = 8;   // k_bin appends work items to 8 segments (workgr
 inline int64_t tc_words(int ntiles) { return (int64_t)ntiles * kTcStride + (3 + kItemSegs) * 32; }
 
 // The per-scene moment tables hold D = n S_bb - S_b^2 (int32) where the
-// scorer stages them in LDS (V <= MVS_TAB_LT_VIEWS: k_score_tab's tile rows;
-// V > 64: k_score_mma_v) and w = 1/sqrt(D) (binary64) otherwise.
-// k_score_tab stages the tile's table rows in LDS up to this V (its VP; A/B
-// switch, 0 = never): measured slower at dinoRing (one buffer set per
-// workgroup: 121 vs 110 us; one workgroup per CU with two sets: 135 us)
-#ifndef MVS_TAB_LT_VIEWS
-#define MVS_TAB_LT_VIEWS 0
-#endif
-inline bool moments_dtab(int V) { return V <= MVS_TAB_LT_VIEWS || V > 64; }
-// k_score_tab A/B switch: the decision's weight gathered as binary32 from a
-// wf table (4 B per (candidate, view) instead of 8) and the binary64 w of the
-// sum only for the passing pairs (4.5 % of them on the bench's sweep), one
-// candidate step after the decision.  Measured slower (120 vs 106 us per
-// 2^20, profiles/r05/r5c_ab_split_implicit.log): off, and no wf table then
-#ifndef MVS_TAB_SPLIT
-#define MVS_TAB_SPLIT 0
-#endif
+// scorer is k_score_mma_v (V > 64) and w = 1/sqrt(D) (binary64, k_score_tab)
+// otherwise.
+inline bool moments_dtab(int V) { return V > 64; }
 
 struct TiledArgs {
     int ntx, nty, ntiles;
@@ -130,40 +116,16 @@ struct TiledArgs {
     // k < ntiles is (tile k, chunk 0) -- tile order without k_item_scan --
     // and k_bin appends the further chunks (tile, j >= 1) to segment 1
     int implicit;
-    // binning without global atomics (MVS_BIN3): bin_rows[b * ntiles + k] =
-    // binning workgroup b's count of tile k, then its first bucket slot there;
-    // bin_scratch[i] = candidate i's (tile, rank in its workgroup | pk << 12);
-    // bin_words ints available (0: k_bin's atomics instead)
-    int32_t* bin_rows;
-    int2* bin_scratch;
-    int64_t bin_words;
+    // direct-path statistics since the context was created (k_score_fix's
+    // finishing workgroup; mvs_scorer_stats): [0] candidates on the direct
+    // path's list, [1] of them bucket overflow (k_bin), [2] batches
+    unsigned long long* stats;
 };
-// candidates per binning workgroup (k_bin, k_bin_count): 1024 threads x
-// MVS_BIN_PER; the host sizes bin_rows by it
+// candidates per binning workgroup (k_bin): 1024 threads x MVS_BIN_PER
 #ifndef MVS_BIN_PER
 #define MVS_BIN_PER 4
 #endif
 #define MVS_BIN_CHUNK (1024 * MVS_BIN_PER)
-// MVS_BIN3: the tiled scorers' binning in three launches without global
-// atomics -- k_bin_count (projection, window test, LDS ranks, the
-// workgroup's tile histogram row), k_bin_scan (per tile, the exclusive
-// prefix of its column over the workgroups, the tile's count and its work
-// items), k_bin_scatter -- instead of k_bin's one returning atomic per
-// (workgroup, tile) (486k of them per 2^20 sweep, ~200 on each counter).
-// A/B switch, off: measured slower, 14.2 + 5.5 + 15.4 = 35 us against k_bin's
-// 27.7-28.0 (profiles/r05/r5m_ab_bin3.log): the scatter alone, now a kernel
-// of its own, costs 15 us -- the bucket writes land as partial lines from
-// every XCD -- where k_bin hides it behind its own chain
-// k_bin A/B switch: two neighbouring tiles' counters per 64-bit returning
-// atomic (~40 % fewer atomics).  Measured slower: 34.3-34.5 vs 27.7-27.9 us
-// (profiles/r05/r5bp_ab_bin_pairs.log)
-#ifndef MVS_BIN_PAIRS
-#define MVS_BIN_PAIRS 0
-#endif
-#ifndef MVS_BIN3
-#define MVS_BIN3 0
-#endif
-
 // Per-scene window moments of the tiled scorers, one table pair per window
 // half-width, built once from the gray stack (k_moments): for pixel (y, x)
 // with a valid window and view v, element (y * W + x) * VP + v holds
@@ -172,18 +134,15 @@ struct TiledArgs {
 //   V <= 64 (k_score_tab, global table reads): w = 1 / sqrt(n S_bb -
 //     S_b^2) (v_rsq_f64 + one Newton step; nan for a constant window and for
 //     the pad views V <= v < VP), VP = 16 ceil(V / 16);
-//   V <= MVS_TAB_LT_VIEWS (A/B switch, off: k_score_tab with the tile's rows
-//     staged in LDS) and V > 64 (k_score_mma_v): D = n S_bb - S_b^2 (int32,
-//     exact; -1 for the pad views; the scorer forms w from D with the same
-//     two instructions), VP = 16 ceil(V / 16) resp. 64 ceil(V / 64).
+//   V > 64 (k_score_mma_v): D = n S_bb - S_b^2 (int32, exact; -1 for the pad
+//     views; the scorer forms w from D with the same two instructions),
+//     VP = 64 ceil(V / 64).
 // The tables hold H W + 16 pixels (a tile row staged whole may run 16 pixels
 // past the last one).
 struct MomentsDev {
     int16_t* sb;
-    double* w;      // 48 < V <= 64
-    float* wf;      // beside w: (float)w, the binary32 weight of k_score_tab's decision (its
-                    // binary64 w is then read only for the views that pass)
-    int32_t* d;     // moments_dtab(V): V <= 48 or V > 64
+    double* w;      // V <= 64
+    int32_t* d;     // moments_dtab(V): V > 64
     int VP;
     int wid;
 };
@@ -225,11 +184,6 @@ struct ExpandArgs {
 #define MVS_MMA_CHUNK 1024    // candidates per work item, V <= 64 (whole tiles, as a rule)
 #define MVS_GROUP_VIEWS 64    // views per group when V > 64
 #define MVS_GROUP_CHUNK 116   // candidates per work item when V > 64 (their reference rows staged)
-// k_acc_pack A/B switch: every candidate's point loaded with its mask word
-// (1) or only the accepted ones' once the counts are in (0)
-#ifndef MVS_ACC_EAGER
-#define MVS_ACC_EAGER 0
-#endif
 #ifndef MVS_ACC_PER
 #define MVS_ACC_PER 8         // candidates per thread of the exchange's pack (A/B switch)
 #endif

@@ -27,19 +27,78 @@
 namespace {
 
 // ctNcc of view R's and view v's windows at (q, r) in numpy's operation order
-// (the guard-band path: rare).  The pixels are read from the stack as the
-// loops need them rather than held in registers, so that the callers
-// (k_score_fix, k_score, k_exact_avg) stay small: no scratch, cheap launches.
+// (the guard-band path: rare).  Both windows' rows come in with every load in
+// flight at once (one memory round trip), aligned to the window's first
+// column (alignbyte) and held as packed bytes; the numpy-order arithmetic
+// then reads every pixel from a register (constant indices: fully unrolled).
+// Reading pixel by pixel from memory in the serial loops cost ~20 us per call
+// (one dependent load per pixel and pass): a single such pair in a sweep set
+// the whole k_score_fix launch (26 us at wid 3, profiles/r06/).
 template <int WID>
 __device__ __noinline__ double exact_ncc_stack(const SceneDev sc, int R, int v, int q, int r) {
-    constexpr int NB = 2 * WID + 1;
+    constexpr int NB = 2 * WID + 1, NPX = NB * NB;
+    constexpr int NW = (NB + 3) / 4, ND = NW + 1;   // aligned dwords per row, dwords loaded per row
     const int64_t vstride = (int64_t)sc.V * 4;
-    const uint8_t* base = sc.stack + (int64_t)(r - WID) * sc.row_bytes;
-    auto px = [&](int view, int i) -> int {
-        const int row = i / NB, col = q - WID + i % NB;
-        return base[(int64_t)row * sc.row_bytes + (int64_t)(col >> 2) * vstride + view * 4 + (col & 3)];
+    const int o = (q - WID) & 3;
+    const uint8_t* p0 = sc.stack + (int64_t)(r - WID) * sc.row_bytes + (int64_t)((q - WID) >> 2) * vstride;
+    // one window's rows, every load in flight, aligned to column q - WID
+    auto window = [&](int view, uint32_t (&w)[NB][NW]) {
+        uint32_t d[NB][ND];
+#pragma unroll
+        for (int row = 0; row < NB; ++row)
+#pragma unroll
+            for (int j = 0; j < ND; ++j)
+                d[row][j] = *(const uint32_t*)(p0 + (int64_t)row * sc.row_bytes + j * vstride + view * 4);
+#pragma unroll
+        for (int row = 0; row < NB; ++row)
+#pragma unroll
+            for (int j = 0; j < NW; ++j) w[row][j] = __builtin_amdgcn_alignbyte(d[row][j + 1], d[row][j], o);
     };
-    return exact_ncc_generic([&](int i) { return px(R, i); }, [&](int i) { return px(v, i); }, NB * NB);
+    uint32_t wa[NB][NW], wb[NB][NW];
+    window(R, wa);
+    __builtin_amdgcn_sched_barrier(0);   // the second window's loads after: fewer registers in flight
+    window(v, wb);
+    // pixel i as a double, re-extracted at every use (opaque): kept as packed
+    // bytes, not as NPX live doubles per window
+    auto px = [&](const uint32_t (&w)[NB][NW], int i) -> double {
+        const uint32_t word = (uint32_t)opaque((int)w[i / NB][(i % NB) >> 2]);
+        return (double)((word >> (8 * ((i % NB) & 3))) & 255u);
+    };
+    int sa = 0, sb = 0;
+#pragma unroll
+    for (int i = 0; i < NPX; ++i) {
+        sa += (int)((wa[i / NB][(i % NB) >> 2] >> (8 * ((i % NB) & 3))) & 255u);
+        sb += (int)((wb[i / NB][(i % NB) >> 2] >> (8 * ((i % NB) & 3))) & 255u);
+    }
+    const double ma = (double)sa / NPX, mb = (double)sb / NPX;
+    // numpy's pairwise sum of (x - mean)^2 for 8 <= n <= 128: 8 accumulators,
+    // combined pairwise, the remainder added in order (as pairwise_sq)
+    static_assert(NPX >= 8 && NPX <= 128, "numpy pairwise summation restated for 8 <= n <= 128");
+    auto pw = [&](const uint32_t (&w)[NB][NW], double m) -> double {
+        double acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const double x = px(w, j) - m; acc[j] = x * x; }
+#pragma unroll
+        for (int i = 8; i < NPX - (NPX % 8); i += 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { const double x = px(w, i + j) - m; acc[j] += x * x; }
+        double res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+        for (int i = NPX - (NPX % 8); i < NPX; ++i) { const double x = px(w, i) - m; res += x * x; }
+        return res;
+    };
+    const double stda = sqrt(pw(wa, ma) / NPX), stdb = sqrt(pw(wb, mb) / NPX);
+    // sum(d1 * d2) with Python's sequential sum (MVS2.py:43)
+    double acc = 0;
+#pragma unroll
+    for (int i = 0; i < NPX; ++i) acc = acc + ((px(wa, i) - ma) / stda) * ((px(wb, i) - mb) / stdb);
+    return acc / (NPX - 1);
+}
+
+DEV int wave_reduce_add(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
 }
 
 DEV double wave_sum(double x) {
@@ -341,7 +400,7 @@ __device__ unsigned long long g_stamps[4096 * 16];
 #endif
 
 constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
-static_assert(kBinBlock * kBinPer == MVS_BIN_CHUNK, "the host sizes bin_rows by MVS_BIN_CHUNK");
+static_assert(kBinBlock * kBinPer == MVS_BIN_CHUNK, "MVS_BIN_CHUNK candidates per k_bin workgroup");
 static_assert(kBinBlock * kBinPer <= 4096, "k_bin_count packs a rank inside the workgroup into 12 bits");
 #ifndef MVS_IMPLICIT_MEAN
 #define MVS_IMPLICIT_MEAN 64   // A/B switch (a huge value keeps k_item_scan everywhere)
@@ -390,7 +449,7 @@ __global__ __launch_bounds__(kScanThreads) void k_item_scan(const TiledArgs t) {
 
 template <bool LDSHIST>
 __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const ScoreArgs a,
-                                                   const TiledArgs t, int wid) {
+                                                   const TiledArgs t, int wid, const MomentsDev mt) {
     extern __shared__ int32_t hist[];      // [ntiles] local counts, then global bases
     // the cameras' projection constants (R', t, fx fy cx cy) in LDS: every
     // candidate reads its reference camera's 16 values there instead of by
@@ -421,10 +480,22 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         ck[k][1] = a.c[3 * ii + 1];
         ck[k][2] = a.c[3 * ii + 2];
     }
+    // a candidate whose reference window is constant (D_a = 0: ctNcc's std is
+    // 0, every view's NCC nan, MVS2.py:41-42) passes no view: its outputs are
+    // written here (V = [], avg 0) and it is not binned, so the scorers never
+    // see it.  Decided from the scene's moment tables (w nan at V <= 64, D = 0
+    // at V > 64), one gather per candidate, all of a thread's in flight
+    const bool flat_test = mt.sb != nullptr && (mt.w != nullptr || mt.d != nullptr);
+    const bool dtab = mt.d != nullptr;
+    double wk[kBinPer];
+    int dk[kBinPer];
+    int qk[kBinPer], rk[kBinPer];
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
         tl[k] = -1;
+        wk[k] = 0.0;
+        dk[k] = 1;
         if (i >= a.n) continue;
         const int R = Rk[k];
         const double c[3] = {ck[k][0], ck[k][1], ck[k][2]};
@@ -439,6 +510,27 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             if (a.avg) a.avg[i * a.astride] = 0.0;
             continue;
         }
+        tl[k] = 0;
+        qk[k] = q;
+        rk[k] = r;
+        if (flat_test) {
+            const int64_t e = ((int64_t)r * sc.W + q) * mt.VP + R;
+            if (dtab) dk[k] = mt.d[e];
+            else wk[k] = mt.w[e];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+        if (tl[k] < 0) continue;
+        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
+        if (flat_test && (dtab ? dk[k] == 0 : wk[k] != wk[k])) {
+            tl[k] = -1;
+            for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
+            if (a.count) a.count[i] = 0;
+            if (a.avg) a.avg[i * a.astride] = 0.0;
+            continue;
+        }
+        const int R = Rk[k], q = qk[k], r = rk[k];
         const int tx = q / MVS_TILE_W, ty = r / MVS_TILE_H;
         const int tile = ty * t.ntx + tx;
         tl[k] = tile;
@@ -458,32 +550,6 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         // returning atomics in flight together (ntiles <= 16 x 1024)
         __syncthreads();
         int bs[kBinLdsTiles / kBinBlock];
-#if MVS_BIN_PAIRS
-        // two neighbouring tiles' counters (one 8-B word) per returning 64-bit
-        // atomic: ~1,150 instead of ~1,900 atomics per workgroup; thread t,
-        // step j takes tiles 2 (t + 1024 j) and 2 (t + 1024 j) + 1
-        static_assert(kTcStride == 1, "tile counter pairs need stride 1");
-#pragma unroll
-        for (int j = 0; j < kBinLdsTiles / kBinBlock / 2; ++j) {
-            const int b = 2 * (threadIdx.x + j * kBinBlock);
-            const int c0 = b < t.ntiles ? hist[b] : 0;
-            const int c1 = b + 1 < t.ntiles ? hist[b + 1] : 0;
-            int o0 = 0, o1 = 0;
-            if (c1 != 0) {
-                const unsigned long long old =
-                    atomicAdd((unsigned long long*)(t.tile_count + b), (unsigned long long)(uint32_t)c0 |
-                                                                           ((unsigned long long)(uint32_t)c1 << 32));
-                o0 = (int)(uint32_t)old;
-                o1 = (int)(old >> 32);
-            } else if (c0 != 0) {
-                o0 = atomicAdd(&t.tile_count[b], c0);
-            }
-            bs[2 * j] = o0;
-            bs[2 * j + 1] = o1;
-        }
-        // bs[2 j + h] is tile 2 (t + 1024 j) + h
-        auto bs_tile = [&](int jj) { return 2 * (threadIdx.x + (jj >> 1) * kBinBlock) + (jj & 1); };
-#else
 #pragma unroll
         for (int j = 0; j < kBinLdsTiles / kBinBlock; ++j) {
             const int b = threadIdx.x + j * kBinBlock;
@@ -491,7 +557,6 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
             bs[j] = c ? atomicAdd(&t.tile_count[b * kTcStride], c) : 0;
         }
         auto bs_tile = [&](int jj) { return (int)threadIdx.x + jj * kBinBlock; };
-#endif
         if (t.implicit) {
             // implicit items: the workgroup whose share of a tile's bucket
             // holds the first entry of chunk j >= 1 (below cap) appends (tile, j)
@@ -532,136 +597,6 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     STAMP_ADD_ROW(2048 + blockIdx.x, 3, t3 - t2);
 }
 
-// Binning without global atomics (MVS_BIN3), stage 1 of 3: k_bin's
-// projection, window test and LDS ranks; the workgroup's tile histogram goes
-// out as one row (rows[b * ntiles + k]) and each candidate's (tile, rank in
-// the workgroup | pk << 12) to the scratch word (tile -1: no valid window).
-__global__ __launch_bounds__(kBinBlock) void k_bin_count(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
-                                                         int wid) {
-    extern __shared__ int32_t hist[];      // [ntiles]
-    __shared__ double s_cam[MVS_MAX_VIEWS][16];
-    const int words = (sc.V + 63) >> 6;
-    for (int k = threadIdx.x; k < sc.V * 16; k += blockDim.x) {
-        const int v = k >> 4, f = k & 15;
-        const CamDev& cm = sc.cams[v];
-        s_cam[v][f] = f < 9 ? cm.Rp[f] : f < 12 ? cm.t[f - 9] : f == 12 ? cm.fx : f == 13 ? cm.fy : f == 14 ? cm.cx : cm.cy;
-    }
-    for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
-    __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
-    int Rk[kBinPer];
-    double ck[kBinPer][3];
-#pragma unroll
-    for (int k = 0; k < kBinPer; ++k) {
-        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        const int64_t ii = i < a.n ? i : 0;
-        Rk[k] = a.ref[ii];
-        ck[k][0] = a.c[3 * ii];
-        ck[k][1] = a.c[3 * ii + 1];
-        ck[k][2] = a.c[3 * ii + 2];
-    }
-    int tl[kBinPer], lr[kBinPer], pk[kBinPer];
-#pragma unroll
-    for (int k = 0; k < kBinPer; ++k) {
-        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        tl[k] = -1;
-        lr[k] = pk[k] = 0;
-        if (i >= a.n) continue;
-        const int R = Rk[k];
-        const double c[3] = {ck[k][0], ck[k][1], ck[k][2]};
-        double px, py;
-        project_vals(s_cam[R], c, px, py);
-        a.xy[2 * i] = px;
-        a.xy[2 * i + 1] = py;
-        int q, r;
-        if (!window_ok(sc, px, py, wid, &q, &r)) {
-            for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
-            if (a.count) a.count[i] = 0;
-            if (a.avg) a.avg[i * a.astride] = 0.0;
-            continue;
-        }
-        const int tx = q / MVS_TILE_W, ty = r / MVS_TILE_H;
-        tl[k] = ty * t.ntx + tx;
-        pk[k] = (q - tx * MVS_TILE_W) | ((r - ty * MVS_TILE_H) << 4) | (R << 7);
-        lr[k] = atomicAdd(&hist[tl[k]], 1);
-    }
-#pragma unroll
-    for (int k = 0; k < kBinPer; ++k) {
-        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        if (i < a.n) t.bin_scratch[i] = make_int2(tl[k], lr[k] | (pk[k] << 12));
-    }
-    __syncthreads();
-    int32_t* row = t.bin_rows + (int64_t)blockIdx.x * t.ntiles;
-    for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) row[b] = hist[b];
-}
-
-// Stage 2 of 3: 64 tiles per workgroup, each tile's column of nbin counts in
-// 16 segments (one wave each); rows become every workgroup's first slot in
-// the tile's bucket, and the tile's total its count.  Implicit items: the
-// tile's chunks j >= 1 below cap are appended to segment 1.
-constexpr int kBinScanSegs = 16;
-__global__ __launch_bounds__(1024) void k_bin_scan(const TiledArgs t, int nbin) {
-    __shared__ int s_seg[kBinScanSegs][65];
-    const int tl = threadIdx.x & 63, sg = threadIdx.x >> 6;
-    const int tile = blockIdx.x * 64 + tl;
-    const int per = (nbin + kBinScanSegs - 1) / kBinScanSegs;
-    const int w0 = min(sg * per, nbin), w1 = min(w0 + per, nbin);
-    int32_t* col = t.bin_rows + tile;
-    int s = 0;
-    if (tile < t.ntiles) {
-        int w = w0;
-        for (; w + 4 <= w1; w += 4)
-            s += col[(int64_t)w * t.ntiles] + col[(int64_t)(w + 1) * t.ntiles] + col[(int64_t)(w + 2) * t.ntiles] +
-                 col[(int64_t)(w + 3) * t.ntiles];
-        for (; w < w1; ++w) s += col[(int64_t)w * t.ntiles];
-    }
-    s_seg[sg][tl] = s;
-    __syncthreads();
-    int pre = 0;
-    for (int q = 0; q < sg; ++q) pre += s_seg[q][tl];
-    if (tile >= t.ntiles) return;
-    for (int w = w0; w < w1; ++w) {
-        const int c = col[(int64_t)w * t.ntiles];
-        col[(int64_t)w * t.ntiles] = pre;
-        pre += c;
-    }
-    if (sg == kBinScanSegs - 1) {
-        const int total = pre;   // the last segment's prefix after its own: the tile's count
-        t.tile_count[tile * kTcStride] = total;
-        if (t.implicit) {
-            const int end = min(total, t.cap);
-            for (int q = 1; q * t.chunk < end; ++q)
-                t.items[t.item_seg + atomicAdd(&t.n_items[32], 1)] = make_int4(tile, q, 0, 0);
-        }
-    }
-}
-
-// Stage 3 of 3: candidate i of workgroup b goes to its tile's bucket at b's
-// first slot + its rank in b (past the bucket's capacity: the direct path's
-// list), the same entries k_bin writes.
-__global__ __launch_bounds__(kBinBlock) void k_bin_scatter(const ScoreArgs a, const TiledArgs t) {
-    const int64_t base = (int64_t)blockIdx.x * kBinBlock * kBinPer;
-    const int32_t* row = t.bin_rows + (int64_t)blockIdx.x * t.ntiles;
-    int2 e[kBinPer];
-#pragma unroll
-    for (int k = 0; k < kBinPer; ++k) {
-        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        e[k] = i < a.n ? t.bin_scratch[i] : make_int2(-1, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < kBinPer; ++k) {
-        const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        const int tile = e[k].x;
-        if (tile < 0) continue;
-        const int pk = e[k].y >> 12;
-        const int rank = row[tile] + (e[k].y & 4095);
-        if (rank < t.cap)
-            t.sorted[(int64_t)tile * t.cap + rank] = make_int2((int32_t)i, pk);
-        else
-            t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)i, tile, pk, 0);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Tiled scorer, stage 2: the candidates of a 16x8 pixel tile against every
 // view on the matrix cores (v_mfma_i32_16x16x64_i8 over the tile's window
@@ -699,12 +634,6 @@ constexpr int kSortBins = MVS_TILE_H / 2;   // k_score_mma sorts an item's candi
 //      k_score_fix (numpy-order ctNcc).  avg_ncc_score = n/(n-1) w_a
 //      sum(num w_b) / cnt in binary64.
 // ---------------------------------------------------------------------------
-#ifdef MVS_DIAG_NOSTORE
-#define MVS_DIAG_STORE_OK(idx) ((idx) == -7)
-#else
-#define MVS_DIAG_STORE_OK(idx) true
-#endif
-
 // a candidate's constants in phase 3 (per wave, 32 slots: the two M-blocks
 // of its unit)
 struct alignas(16) CandInfo {
@@ -1311,16 +1240,9 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma(const SceneDev sc, co
                         mk &= ~(1ull << Rv[h]);
                         const int cnt = __popcll(mk);
                         const int64_t idx = e[h].x;
-    #ifdef MVS_DIAG_NOSTORE
-                        // diagnostic build: the outputs computed, not stored
-                        if (idx == -7) {
-    #else
-                        {
-    #endif
                         a.mask[idx * a.mstride] = mk;
                         if (a.count) a.count[idx] = cnt;
-                        }
-                        if (a.avg && MVS_DIAG_STORE_OK(idx)) {
+                        if (a.avg) {
                             // its own term num_RR w_a = D_a w_a = sqrt(D_a) = 1 / w_a (to
                             // the rsq + Newton accuracy of w_a, 4e-15) leaves the sum
                             double inv = __builtin_amdgcn_rcp(my_wa[h]);
@@ -1674,12 +1596,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             if (g == 0 && tid == 0) claim = atomicAdd(head, 1);
             // ---- 2. Q = S_bb of every (pixel, view) of the group ----
             // (TAB: none, the scene's tables hold S_b and D)
-#ifdef MVS_DIAG_NOPHASE2
-            if (false) {
-#else
             if (TAB) {
             } else if (mv < GV) {
-#endif
                 // rows in order, the window sliding down as they come: at most
                 // NB + 1 row sums live
                 int Q[ROWS];
@@ -1787,14 +1705,6 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                 // region row 2s + (kh >> 1) = window row 2s + (kh >> 1) - rrel of the candidate
                 const int aoff = (min(kk, nc - 1) * NB - rrel) * 32 + 16 * (kh & 1);
                 const int ioff = qrel * 32 + 16 * (kh & 1);
-#ifdef MVS_DIAG_AISEL
-                uint32_t cmi[4];
-                {
-                    const uint32_t hm = (valid ? (((1u << NB) - 1u) << (qrel + C0)) : 0u) >> (16 * (kh & 1));
-#pragma unroll
-                    for (int k4 = 0; k4 < 4; ++k4) cmi[k4] = byte_mask((hm >> (4 * k4)) & 15u) & 0x01010101u;
-                }
-#endif
                 const uint8_t* bptr0 = reg + min(32 * h + m, GV - 1) * VS + lofs;
                 const uint8_t* bptr1 = reg + min(32 * h + 16 + m, GV - 1) * VS + lofs;
                 v4i C0v = {0, 0, 0, 0}, C1v = {0, 0, 0, 0}, S0v = {0, 0, 0, 0}, S1v = {0, 0, 0, 0};
@@ -1804,12 +1714,8 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                     // rows outside the window read 16 zero bytes: an offset select
                     // instead of a branch around the load
                     const uint4 av = *(const uint4*)(s_areg + (rv ? aoff + row * 32 : AZERO));
-#ifdef MVS_DIAG_AISEL
-                    const v4i AI = rv ? (v4i){(int)cmi[0], (int)cmi[1], (int)cmi[2], (int)cmi[3]} : (v4i){0, 0, 0, 0};
-#else
                     const uint4 iv = *(const uint4*)(s_ind + (rv ? ioff : 16 * 32));
                     const v4i AI = {(int)iv.x, (int)iv.y, (int)iv.z, (int)iv.w};
-#endif
                     const v4i A = {(int)av.x, (int)av.y, (int)av.z, (int)av.w};
                     const uint4 b0 = *(const uint4*)(bptr0 + 64 * s);
                     const uint4 b1 = *(const uint4*)(bptr1 + 64 * s);
@@ -1880,11 +1786,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                         pmv = writelane<2 * (2 * i + j)>(pmv, (uint32_t)P);
                         pmv = writelane<2 * (2 * i + j) + 1>(pmv, (uint32_t)(P >> 32));
                         gacc |= Gd;
-#ifdef MVS_DIAG_SASEL
-                        sa = fma((double)num, __builtin_amdgcn_inverse_ballot_w64(P) ? w : 0.0, sa);
-#else
                         sa = fma_f64_lanes(sa, num, w, P);
-#endif
                     });
                     gdv = writelane<2 * i>(gdv, (uint32_t)gacc);
                     gdv = writelane<2 * i + 1>(gdv, (uint32_t)(gacc >> 32));
@@ -1979,7 +1881,17 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
     const int nfix = *t.fix_count;
     const int active = nfix > kFixSmall ? (int)gridDim.x : kFixBase;   // uniform over the grid
     if ((int)blockIdx.x >= active) return;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += active * 256) t.tile_count[k * kTcStride] = 0;
+    // the tile counters back to zero; the bucket overflow (candidates past a
+    // tile's cap, which k_bin put on the list) counted on the way
+    int over = 0;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += active * 256) {
+        over += max(t.tile_count[k * kTcStride] - t.cap, 0);
+        t.tile_count[k * kTcStride] = 0;
+    }
+    if (t.stats && __syncthreads_or(over != 0)) {
+        over = wave_reduce_add(over);
+        if ((threadIdx.x & 63) == 0 && over) atomicAdd(&t.stats[1], (unsigned long long)over);
+    }
     for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
          k += active * 4) {
         const int4 f = t.fix_list[k];
@@ -1993,6 +1905,10 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
     }
     __syncthreads();
     if (threadIdx.x == 0 && atomicAdd(t.done, 1) == active - 1) {
+        if (t.stats) {
+            t.stats[0] += (unsigned long long)nfix;
+            t.stats[2] += 1ull;
+        }
         *t.fix_count = 0;
         for (int x = 0; x < kItemSegs; ++x) t.n_items[32 * x] = 0;
         *t.head = 0;
@@ -2287,27 +2203,11 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             }
         }
         double px[kAccPer], py[kAccPer], pz[kAccPer];
-#if MVS_ACC_EAGER
-        // every candidate's point in flight with its mask word (no round trip
-        // between the counts and the points; the rejected ones' are dropped)
-#pragma unroll
-        for (int j = 0; j < kAccPer; ++j) {
-            const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            px[j] = py[j] = pz[j] = 0.0;
-            if (cpt && i < n) {
-                const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
-                px[j] = xy.x;
-                py[j] = xy.y;
-                pz[j] = cpt[3 * i + 2];
-            }
-        }
-#endif
 #pragma unroll
         for (int j = 0; j < kAccPer; ++j) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
             const bool acc = i < n && c[j] >= vlb;
             m[j] = __ballot(acc);
-#if !MVS_ACC_EAGER
             px[j] = py[j] = pz[j] = 0.0;
             if (cpt && acc) {
                 // x, y as one 16-B load (8-B aligned), z beside it
@@ -2316,7 +2216,6 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
                 py[j] = xy.y;
                 pz[j] = cpt[3 * i + 2];
             }
-#endif
             if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
         }
         lds_barrier();   // the points stay in flight
@@ -2676,16 +2575,13 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     // tiles themselves as its items, in tile order, and needs no k_item_scan
     TiledArgs tv = *t;
     tv.implicit = (!grouped && mt && a->n >= (int64_t)kImplicitMean * t->ntiles) ? 1 : 0;
-    const bool bin3 = MVS_BIN3 && t->ntiles <= kBinLdsTiles && t->bin_rows && t->bin_scratch &&
-                      (int64_t)nbin * t->ntiles + 2 * a->n <= t->bin_words;
-    if (bin3) {
-        hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, tv, WID);
-        hipLaunchKernelGGL(k_bin_scan, dim3((t->ntiles + 63) / 64), dim3(1024), 0, s, tv, nbin);
-        hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(kBinBlock), 0, s, *a, tv);
-    } else if (t->ntiles <= kBinLdsTiles)
-        hipLaunchKernelGGL(k_bin<true>, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, tv, WID);
+    // with the scene's moment tables k_bin also settles the candidates whose
+    // reference window is constant (they pass no view) without binning them
+    const MomentsDev mflat = mt ? *mt : MomentsDev{};
+    if (t->ntiles <= kBinLdsTiles)
+        hipLaunchKernelGGL(k_bin<true>, dim3(nbin), dim3(kBinBlock), (size_t)t->ntiles * 4, s, *sc, *a, tv, WID, mflat);
     else
-        hipLaunchKernelGGL(k_bin<false>, dim3(nbin), dim3(kBinBlock), 0, s, *sc, *a, tv, WID);
+        hipLaunchKernelGGL(k_bin<false>, dim3(nbin), dim3(kBinBlock), 0, s, *sc, *a, tv, WID, mflat);
     // the work items in tile order (the scorers' workgroups in flight then
     // share image rows -- and at V > 64 table rows -- in L2)
     if (!tv.implicit) hipLaunchKernelGGL(k_item_scan, dim3(1), dim3(kScanThreads), 0, s, tv);

@@ -18,10 +18,6 @@
 #include "mvs_device.h"
 #include "mvs_mma.h"
 
-// k_score_tab's SPLIT gather leaves the binary64 weight of a failing lane
-// unset on purpose (its sum term is masked off)
-#pragma clang diagnostic ignored "-Wsometimes-uninitialized"
-
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -112,14 +108,12 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
                     double w = __builtin_amdgcn_rsq(D);
                     w = w * (1.5 - 0.5 * D * w * w);
                     mt.w[o] = w;
-                    if (mt.wf) mt.wf[o] = (float)w;
                 }
             } else {
                 mt.sb[o] = 0;
                 if constexpr (DTAB) mt.d[o] = -1;
                 else {
                     mt.w[o] = __builtin_nan("");
-                    if (mt.wf) mt.wf[o] = __builtin_nanf("");
                 }
             }
         }
@@ -165,127 +159,23 @@ __device__ unsigned long long g_stamps_tab[1024 * 16];
 #define TSTAMP_ADD(slot, val)
 #endif
 
-// MVS_TAB_ONE (A/B switch): one workgroup per CU with all 160 KiB of LDS (two
-// waves per SIMD, 256 VGPRs each): region, list and table rows double-buffered
-#ifndef MVS_TAB_ONE
-#define MVS_TAB_ONE 0
-#endif
-#ifndef MVS_TAB_PIXSORT
-#define MVS_TAB_PIXSORT 0   // A/B switch: sort a wave's candidates by pixel, not by row pair
-#endif
-// MVS_TAB_SPLIT (A/B switch, mvs_internal.h): measured slower, 120 vs 106 us
-// per 2^20 (profiles/r05/r5c_ab_split_implicit.log)
-// MVS_TAB_TR (A/B switch): the MFMA's operands swapped, so that lane (kh, m)
-// holds candidate m's window products for views 16 nb + 4 kh + r: each lane
-// decides for its own candidate, gathers its table entries as 8- and 32-byte
-// runs (3 loads per view block instead of 8), builds its part of the mask
-// word in a register, and four-lane permlane swaps finish mask, sum and
-// guard (no v_writelane, no row reduction).  Measured slower, 115-117 vs
-// 103.5-104.6 us per 2^20 (profiles/r05/r5e_ab_transposed.log): its first
-// table use waits for the next item's LDS-DMA too (the compiler does not
-// order the two kinds of load, so every such wait is a vmcnt(0)), and the
-// loads issued before the K-loop instead spill at 4 waves per SIMD
-#ifndef MVS_TAB_TR
-#define MVS_TAB_TR 0
-#endif
-// MVS_TAB_DMA_WAVES (A/B switch): only the last this-many waves issue the next
-// item's LDS-DMA.  A wave's wait for any load issued after a pending LDS-DMA
-// is a vmcnt(0) (the compiler does not order the two kinds), so the waves
-// that issue none never wait for the next item's region at their table
-// gathers; the issuing waves take the DMA's instruction cost
-#ifndef MVS_TAB_DMA_WAVES
-#define MVS_TAB_DMA_WAVES 64   // all of the workgroup's waves
-#endif
-// MVS_TAB_DMA_LATE (A/B switch): a wave issues its part of the next item's
-// LDS-DMA after its first unit instead of at the round's start, so that its
-// first unit's table gathers do not wait for the DMA (see above)
-#ifndef MVS_TAB_DMA_LATE
-#define MVS_TAB_DMA_LATE 0
-#endif
-#ifndef MVS_TAB_WHATIF
-#define MVS_TAB_WHATIF 0
-#endif
-// MVS_TAB_D64 (A/B switch): the FAST decision in binary64 -- x = fma(num,
-// w_b, -T) on the exact num (one conversion shared with the sum) instead of
-// binary32 copies of num and w_b: 8 VALU per (candidate, view) instead of 10.
-// Outside the guard band both decide as exact arithmetic does (108 GPU tests
-// green with it).  Measured no faster: 104.9-106.1 vs 103.4-106.5 us, with
-// MAXSUM 108.0-108.3 (profiles/r05/r5k_*, r5l_*); the what-if builds
-// (MVS_TAB_WHATIF) put the table gathers at ~11 % of the scorer's time
-#ifndef MVS_TAB_D64
-#define MVS_TAB_D64 0
-#endif
-// MVS_TAB_MAXSUM (with D64): the passing terms summed as max(x, 0), and
-// (passing views) x T added once per candidate: num w_b = x + T for a
-// passing pair up to one rounding of x (well inside avg's 1e-12), with no
-// EXEC change per (candidate, view)
-#ifndef MVS_TAB_MAXSUM
-#define MVS_TAB_MAXSUM 1
-#endif
-// MVS_TAB_TIXV (A/B switch): the table rows of a lane's four candidate steps
-// read as one 16-B LDS load per M-block after the K-loop (a per-wave copy of
-// the tix column), so that no step's gathers wait for an LDS read of their
-// address.  Measured the same: 103.1-105.5 vs 103.3-103.5 us (r5n_*)
-#ifndef MVS_TAB_TIXV
-#define MVS_TAB_TIXV 0
-#endif
-#ifndef MVS_TAB_NOPAD
-#define MVS_TAB_NOPAD 1
-#endif
-#ifndef MVS_TAB_STATIC_FIRST
-#define MVS_TAB_STATIC_FIRST 1
-#endif
-// MVS_TAB_TAIL_SPLIT: the last this-many tiles of a dense batch's implicit
-// items are queued as two half-items each (the first and the second half of
-// the tile's M-blocks; the region staged for both), so that the kernel's
-// last items -- which set its end -- are half as long
-#ifndef MVS_TAB_TAIL_SPLIT
-#define MVS_TAB_TAIL_SPLIT 0
-#endif
-// MVS_TAB_SHALLOW: a workgroup claims item k+2 while it scores item k (the
-// index goes round through LDS at the next round's barrier) instead of item
-// k+3 with item k+2's descriptor already loaded: one item fewer held back
-// when the queue runs dry, so the kernel's tail -- workgroups still working
-// off items they claimed early -- is one item shorter.  An implicit item's
-// descriptor is computed, not loaded, so nothing waits for it
-#ifndef MVS_TAB_SHALLOW
-#define MVS_TAB_SHALLOW 1
-#endif
-// MVS_TAB_LATE_CLAIM (with SHALLOW): thread 0 claims item k+2 after wave 0's
-// first unit of item k (1) or after its last (2) instead of at the round's
-// start (0): less held back when the queue runs dry.  1: 87.95-88.4 vs
-// 90.5-91.4 us (r5x_ab_late_claim.log)
-#ifndef MVS_TAB_LATE_CLAIM
-#define MVS_TAB_LATE_CLAIM 1
-#endif
-// MVS_TAB_WAVES (A/B switch): waves per workgroup (two workgroups per CU).
-// 10 (5 per SIMD, 96 VGPRs with spills): 134.6-135.4 vs 88.4 us (r5wv_*)
-#ifndef MVS_TAB_WAVES
-#define MVS_TAB_WAVES 8
-#endif
-constexpr int kTabThreads = 64 * MVS_TAB_WAVES, kTabWaves = kTabThreads / 64, kTabGrid = MVS_TAB_ONE ? 256 : 512;
-constexpr int kTabBudget = MVS_TAB_ONE ? 160 * 1024 - 1024 : 80 * 1024 - 512;   // LDS bytes per workgroup
-constexpr int kTabMinWaves = MVS_TAB_ONE ? 2 : (2 * kTabWaves + 3) / 4;            // per SIMD
+// The A/B variants measured against this kernel in rounds 4-5 (split and
+// transposed epilogues, binary64 decisions, pixel sorts, LDS table rows, DMA
+// issue by fewer waves or later, 10 waves, tail-split items, one workgroup
+// per CU, ...) are in DESIGN.md 4.1 with their logs under profiles/r05/; the
+// code of each is in the git history (round 5), not in this file.
+constexpr int kTabWaves = 8, kTabThreads = 64 * kTabWaves, kTabGrid = 512;
+constexpr int kTabBudget = 80 * 1024 - 512;                 // LDS bytes per workgroup (two per CU)
+constexpr int kTabMinWaves = (2 * kTabWaves + 3) / 4;       // per SIMD
 constexpr int kTabChunk = MVS_MMA_CHUNK;
 
 // a candidate's constants in a unit (per wave, 32 slots)
 struct alignas(16) TabInfo {
     int32_t tix;   // table element of its pixel, view 0
     int32_t Sa;    // -S_a
-#if MVS_TAB_D64
-    double T;      // FAST: decision threshold on num w_b; else the reference view (-1: no candidate)
-#else
     int32_t R;     // reference view (-1: no candidate)
     float T;       // decision threshold on num w_b (FAST)
-#endif
 };
-#if MVS_TAB_D64
-DEV void ti_set_R(TabInfo& t, int R) { t.T = (double)R; }
-DEV int ti_R(const TabInfo& t) { return (int)t.T; }
-#else
-DEV void ti_set_R(TabInfo& t, int R) { t.R = R; }
-DEV int ti_R(const TabInfo& t) { return t.R; }
-#endif
 
 template <int WID, int NBLK>
 struct TabGeom {
@@ -293,24 +183,11 @@ struct TabGeom {
     static constexpr int RB = VP * MmaGeom<WID>::VS;    // one region buffer (+16 zero bytes)
     static constexpr int CB = kTabChunk * 8;            // one candidate buffer
     static constexpr int FIXED = kTabWaves * 32 * (int)sizeof(TabInfo) + 65 * 8 + 64;
-    // LT: the tile's table rows (S_b int16, D int32 of 8 rows x 16 pixels x
-    // VP views) staged in LDS next to one region and list buffer, where two
-    // workgroups per CU still fit (80 KiB each): V <= 48 at every WID
-    static constexpr int TS = 8 * 16 * VP * 2, TD = 8 * 16 * VP * 4;
-    static constexpr int BUF = (RB + 16) + CB + (VP <= MVS_TAB_LT_VIEWS ? TS + TD : 0);   // one item's LDS
-    static constexpr bool LT = VP <= MVS_TAB_LT_VIEWS;
+    static constexpr int BUF = (RB + 16) + CB;          // one item's LDS
     static_assert(BUF + FIXED <= kTabBudget, "one item's buffers fit");
     // two buffer sets where they fit: item k+1's lands while item k is scored
     static constexpr bool DB = 2 * BUF + FIXED <= kTabBudget;
 };
-
-// w = 1/sqrt(D): the two instructions k_moments uses for its w table (bit
-// for bit the same value)
-DEV double w_of(int db) {
-    const double D = (double)db;
-    const double w = __builtin_amdgcn_rsq(D);
-    return w * (1.5 - 0.5 * D * w * w);
-}
 
 template <int WID, int NBLK, bool FAST>
 __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const SceneDev sc, const ScoreArgs a, const TiledArgs t,
@@ -320,12 +197,10 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     using TG = TabGeom<WID, NBLK>;
     constexpr int NB = G::NB, NPX = G::NPX, KS = G::KS, VS = G::VS, C0 = G::C0;
     constexpr int VP = TG::VP;
-    constexpr bool DB = TG::DB, LT = TG::LT;
+    constexpr bool DB = TG::DB;
 
     constexpr int RPV = VS / 32;                                          // region rows per view incl. the pad row
-    constexpr int DW = MVS_TAB_DMA_WAVES < kTabWaves ? MVS_TAB_DMA_WAVES : kTabWaves, DT = DW * 64;   // the DMA's waves and threads
-    static_assert(DW >= 1 && DW <= kTabWaves, "DMA waves");
-    constexpr int PF = (VP * RPV * 2 + DT - 1) / DT;                      // 16-B pieces per DMA thread
+    constexpr int PF = (VP * RPV * 2 + kTabThreads - 1) / kTabThreads;    // 16-B pieces per thread
     constexpr int RB = TG::RB, CB = TG::CB;
     // distinct LDS objects per buffer: reads of one do not wait for the
     // LDS-DMA into the other; each region buffer ends in 16 zero bytes (rows
@@ -333,9 +208,6 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     __shared__ __attribute__((aligned(16))) uint8_t s_reg0[RB + 16], s_reg1[DB ? RB + 16 : 16];
     __shared__ __attribute__((aligned(16))) uint8_t s_cand0[CB], s_cand1[DB ? CB : 16];
     __shared__ __attribute__((aligned(16))) TabInfo s_ti[kTabWaves * 32];
-    __shared__ __attribute__((aligned(16))) int32_t s_tix[MVS_TAB_TIXV ? kTabWaves * 32 : 4];
-    // LT: the tile's table rows, [S_b rows][D rows]
-    __shared__ __attribute__((aligned(16))) uint8_t s_tab0[LT ? TG::TS + TG::TD : 16], s_tab1[LT && DB ? TG::TS + TG::TD : 16];
     __shared__ int s_ids[2];
     __shared__ double s_recip[65];
 #ifdef MVS_STAMPS
@@ -352,73 +224,34 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
 
     const double kn = (double)NPX / (double)(NPX - 1);
     const float tqf = (float)(a.thr / kn);
-#if MVS_TAB_D64
-    const double tqd = a.thr / kn;
-#endif
     ItemMap im;
     im.load(t);
     // implicit items: k < ntiles is (tile k, chunk 0), then segment 1's
     // further chunks (k_bin); else k_item_scan's list
     const bool implicit = t.implicit != 0;
-    // half-item code in bits 20+ of an item's chunk field: 0 whole, 1 / 2 = first / second half
-    const int tsplit = implicit ? min(MVS_TAB_TAIL_SPLIT, t.ntiles) : 0;
-    const int tsplit0 = t.ntiles - tsplit;
-    const int n_units = implicit ? t.ntiles + tsplit + t.n_items[32] : im.total();
+    const int n_units = implicit ? t.ntiles + t.n_items[32] : im.total();
     int32_t* head = t.head;
     const int16_t* __restrict__ tsb = mt.sb;
     const double* __restrict__ tw = mt.w;
-    const float* __restrict__ twf = mt.wf;
-    constexpr bool SPLIT = FAST && !LT && MVS_TAB_SPLIT;
-    constexpr bool TR = FAST && !LT && !SPLIT && MVS_TAB_TR;
 
     auto region_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_reg1 : s_reg0; };
     auto cand_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_cand1 : s_cand0; };
-    auto tab_buf = [&](auto bufc) -> uint8_t* { return decltype(bufc)::value ? s_tab1 : s_tab0; };
     // the item's region (gv rows) and sorted (id, pk) entries by LDS-DMA
     auto stage = [&](const int4 d, auto bufc) {
-        if (wave < kTabWaves - DW) return;                 // not one of the DMA's waves
-        const int wd = wave - (kTabWaves - DW), td = tid - (kTabWaves - DW) * 64;
         const int ty = d.x / t.ntx, tx = d.x - ty * t.ntx;
         const int x0 = tx * MVS_TILE_W, yr0 = ty * MVS_TILE_H - WID;
         uint8_t* base = region_buf(bufc);
-        if constexpr (!(MVS_TAB_WHATIF & 16))   // measurement only: no region DMA
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
-            const int k = opaque(td) + p * DT;   // recomputed per piece: no long-lived offsets
+            const int k = opaque(tid) + p * kTabThreads;   // recomputed per piece: no long-lived offsets
             const int v = k / (2 * RPV), r2 = k - v * (2 * RPV);
-            // MVS_TAB_NOPAD: the pad row (never read) is not loaded (its lanes masked)
-            if (k < npiece && (!MVS_TAB_NOPAD || (r2 >> 1) != RPV - 1)) {
+            // the pad row (never read) is not loaded (its lanes masked)
+            if (k < npiece && (r2 >> 1) != RPV - 1) {
                 const int y = min(max(yr0 + (r2 >> 1), 0), sc.H - 1);
                 const uint8_t* src = sc.gv + ((int64_t)v * sc.H + y) * sc.Wp + (x0 - 8) + 16 * (r2 & 1);
                 __builtin_amdgcn_global_load_lds((const void*)src,
-                                                 (void __attribute__((address_space(3)))*)(base + (p * DT + wd * 64) * 16),
+                                                 (void __attribute__((address_space(3)))*)(base + (p * kTabThreads + wave * 64) * 16),
                                                  16, 0, 0);
-            }
-        }
-        if constexpr (LT) {
-            // the tile's 8 rows of 16 pixels x VP views, S_b then D: each row
-            // one contiguous run of the tables (rows past H clamped; their
-            // pixels hold no candidate)
-            constexpr int PS = 2 * VP, PD = 4 * VP, NPT = 8 * (PS + PD);   // 16-B pieces
-            const int yt0 = ty * MVS_TILE_H;
-#pragma unroll
-            for (int p = 0; p < (NPT + DT - 1) / DT; ++p) {
-                const int k = opaque(td) + p * DT;
-                if (k < NPT) {
-                    const uint8_t* src;
-                    if (k < 8 * PS) {
-                        const int r = k / PS, c = k - r * PS;
-                        const int64_t px = (int64_t)min(yt0 + r, sc.H - 1) * sc.W + x0;
-                        src = (const uint8_t*)(mt.sb + px * VP) + 16 * c;
-                    } else {
-                        const int k2 = k - 8 * PS, r = k2 / PD, c = k2 - r * PD;
-                        const int64_t px = (int64_t)min(yt0 + r, sc.H - 1) * sc.W + x0;
-                        src = (const uint8_t*)(mt.d + px * VP) + 16 * c;
-                    }
-                    __builtin_amdgcn_global_load_lds((const void*)src,
-                                                     (void __attribute__((address_space(3)))*)(tab_buf(bufc) + (p * DT + wd * 64) * 16),
-                                                     16, 0, 0);
-                }
             }
         }
         // the list in 16-B pieces (two entries; bucket starts are 512-B
@@ -426,25 +259,25 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         uint8_t* cbase = cand_buf(bufc);
         const uint8_t* csrc = (const uint8_t*)(sorted + d.y);
 #pragma unroll
-        for (int p = 0; p < (kTabChunk / 2 + DT - 1) / DT; ++p) {
-            const int k = td + p * DT;
+        for (int p = 0; p < (kTabChunk / 2 + kTabThreads - 1) / kTabThreads; ++p) {
+            const int k = tid + p * kTabThreads;
             if (k < d.w / 2)
                 __builtin_amdgcn_global_load_lds((const void*)(csrc + 16 * k),
-                                                 (void __attribute__((address_space(3)))*)(cbase + (p * DT + wd * 64) * 16),
+                                                 (void __attribute__((address_space(3)))*)(cbase + (p * kTabThreads + wave * 64) * 16),
                                                  16, 0, 0);
         }
     };
 
-    // MVS_TAB_STATIC_FIRST: workgroup b's first two items are b and b + grid
-    // (no claim), the queue hands out the rest -- at the kernel's start the
-    // grid's 2 x 512 claims would otherwise queue on the one head counter
-    const int first = MVS_TAB_STATIC_FIRST ? 2 * (int)gridDim.x : 0;
+    // workgroup b's first two items are b and b + grid (no claim), the queue
+    // hands out the rest -- at the kernel's start the grid's 2 x 512 claims
+    // would otherwise queue on the one head counter
+    const int first = 2 * (int)gridDim.x;
     auto claim = [&]() -> int { return atomicAdd(head, 1) + first; };
     // an item's descriptor (tile, first bucket entry, count, entries staged):
     // the list is staged as a whole chunk (bounded by the bucket), so that its
     // LDS-DMA needs no count -- the count arrives a round later
     auto desc = [&](int2 it, int cnt) -> int4 {
-        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y & 0xfffff);
+        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y);
         const int c = __builtin_amdgcn_readfirstlane(cnt);
         return make_int4(tile, tile * t.cap + j * t.chunk, min(min(c, t.cap) - j * t.chunk, t.chunk),
                          min(t.chunk, t.cap - j * t.chunk));
@@ -454,45 +287,35 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     // read of the round
     auto item_v = [&](int v) -> int2 {
         // the load is issued either way (its wait stays the round end's vmcnt)
-        const int2 ld = *(const int2*)(items + opaque(implicit ? t.item_seg + max(v - t.ntiles - tsplit, 0) : im.slot(v)));
-        if (implicit && v < tsplit0) return make_int2(v, 0);
-        if (implicit && v < t.ntiles + tsplit)
-            return make_int2(tsplit0 + ((v - tsplit0) >> 1), (1 + ((v - tsplit0) & 1)) << 20);
+        const int2 ld = *(const int2*)(items + opaque(implicit ? t.item_seg + max(v - t.ntiles, 0) : im.slot(v)));
+        if (implicit && v < t.ntiles) return make_int2(v, 0);
         return ld;
     };
     auto count_v = [&](int tile) -> int { return t.tile_count[opaque(tile * kTcStride)]; };
     // the item pipeline: while item k is scored, item k+1's region and list
-    // (DB) and its tile's count, item k+2's (tile, chunk) and thread 0's claim
-    // of item k+3 are in flight
+    // (DB) and its tile's count are in flight, and thread 0 claims item k+2
+    // after wave 0's first unit of item k (the index goes round through LDS at
+    // the next round's barrier)
     if (tid == 0) {
-        s_ids[0] = MVS_TAB_STATIC_FIRST ? (int)blockIdx.x : claim();
-        s_ids[1] = MVS_TAB_STATIC_FIRST ? (int)(blockIdx.x + gridDim.x) : claim();
+        s_ids[0] = (int)blockIdx.x;
+        s_ids[1] = (int)(blockIdx.x + gridDim.x);
     }
     __syncthreads();
     int cur = __builtin_amdgcn_readfirstlane(s_ids[0]);
     int nx1 = __builtin_amdgcn_readfirstlane(s_ids[1]);
     if (cur >= n_units) return;
     int4 dcur;
-    int hcur = 0;   // half-item code of the current item
     {
         // an implicit item needs no load; the first DMA needs no count (its
         // list is staged as a whole chunk), so it goes out before the count
-        const int2 it = implicit && cur < tsplit0 ? make_int2(cur, 0) : item_v(cur);
-        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y & 0xfffff);
-        hcur = __builtin_amdgcn_readfirstlane(it.y >> 20);
+        const int2 it = implicit && cur < t.ntiles ? make_int2(cur, 0) : item_v(cur);
+        const int tile = __builtin_amdgcn_readfirstlane(it.x), j = __builtin_amdgcn_readfirstlane(it.y);
         stage(make_int4(tile, tile * t.cap + j * t.chunk, 0, min(t.chunk, t.cap - j * t.chunk)),
               std::integral_constant<int, 0>{});
         dcur = desc(it, count_v(it.x));
     }
-#if MVS_TAB_SHALLOW
     int2 it1 = make_int2(0, 0);
     int pend = nx1;   // thread 0's: the next item, published at round 0's barrier
-#else
-    int2 it1 = nx1 >= n_units ? make_int2(0, 0) : implicit && nx1 < tsplit0 ? make_int2(nx1, 0) : item_v(nx1);
-    it1 = make_int2(__builtin_amdgcn_readfirstlane(it1.x), __builtin_amdgcn_readfirstlane(it1.y));
-    int pend = 0;
-    if (tid == 0) pend = claim();
-#endif
     __syncthreads();   // everyone has read s_ids before they are rewritten
 
     auto round = [&](auto bufc) -> bool {
@@ -500,8 +323,6 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         const int nc = dcur.z;
         const uint8_t* reg = region_buf(bufc);
         int2* cand = (int2*)cand_buf(bufc);
-        const int16_t* ls_sb = (const int16_t*)tab_buf(bufc);
-        const int32_t* ls_d = (const int32_t*)(tab_buf(bufc) + (LT ? TG::TS : 0));
         const int zoff = RB;   // the zero row, relative to the region buffer
         // ---- 1. this item's region and list have landed (every wave's DMA) ----
         TSTAMP(ts0);
@@ -509,78 +330,48 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's LDS-DMA, before the barrier
         __syncthreads();
         TSTAMP(ts1);
-#if MVS_TAB_SHALLOW
         // item k+1 (claimed last round), its region and list into the other
-        // buffer and its count; thread 0's claim of item k+2
+        // buffer and its count
         nx1 = __builtin_amdgcn_readfirstlane(s_ids[0]);
         if (nx1 < n_units) {
             const int2 iv = item_v(nx1);   // implicit: computed; else a load waited for here
             it1 = make_int2(__builtin_amdgcn_readfirstlane(iv.x), __builtin_amdgcn_readfirstlane(iv.y));
         }
-#else
-        const int nx2 = __builtin_amdgcn_readfirstlane(s_ids[0]);
-        // item k+2's (tile, chunk) and item k+1's count (consumed at the
-        // round's end), item k+1's region and list into the other buffer,
-        // thread 0's claim of the one after that
-#endif
-        const int j1 = it1.y & 0xfffff;
+        const int j1 = it1.y;
         const int4 dst1 = make_int4(it1.x, it1.x * t.cap + j1 * t.chunk, 0, min(t.chunk, t.cap - j1 * t.chunk));
-        if constexpr (DB && !MVS_TAB_DMA_LATE) {
+        if constexpr (DB) {
             if (nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
         }
-#if MVS_TAB_SHALLOW
         const int c1 = count_v(it1.x);
-        if (!MVS_TAB_LATE_CLAIM && nx1 < n_units && tid == 0) pend = claim();
-#else
-        // unconditional (clamped) loads: no branch, no register reset that
-        // would wait for the LDS-DMA just issued
-        const int2 it2 = item_v(min(nx2, n_units - 1));
-        const int c1 = count_v(it1.x);
-        if (nx2 < n_units && tid == 0) pend = claim();
-#endif
         TSTAMP(ts1b);
         TSTAMP_ADD(7, ts1b - ts1);
         const int ty = dcur.x / t.ntx, tx = dcur.x - ty * t.ntx;
         const int tix0 = ((ty * MVS_TILE_H) * sc.W + tx * MVS_TILE_W) * VP;   // table element of the tile origin
         // ---- 2. this wave's M-blocks, sorted by row pair inside the wave ----
-        const int nblk_all = (nc + 15) >> 4;
-        // a half-item: its half of the M-blocks
-        const int blo = hcur == 2 ? nblk_all >> 1 : 0, bhi = hcur == 1 ? nblk_all >> 1 : nblk_all;
-        const int nblk = bhi - blo;
-        const int b0 = blo + nblk * wave / kTabWaves, b1 = blo + nblk * (wave + 1) / kTabWaves;
+        const int nblk = (nc + 15) >> 4;
+        const int b0 = nblk * wave / kTabWaves, b1 = nblk * (wave + 1) / kTabWaves;
         {
             const int base = 16 * b0, cnt = min(16 * b1, nc) - base;   // <= 128
-            // one stable counting pass by the digit (pk >> SH) & (NBINS - 1)
-            // (ballots + mbcnt, in the wave's own part of the list)
-            auto pass = [&](auto shc, auto nbc) {
-                constexpr int SH = decltype(shc)::value, NBINS = decltype(nbc)::value;
-                int2 c0 = make_int2(0, 0), c1 = make_int2(0, 0);
-                int bin0 = NBINS, bin1 = NBINS;
-                if (lane < cnt) { c0 = cand[base + lane]; bin0 = (c0.y >> SH) & (NBINS - 1); }
-                if (lane + 64 < cnt) { c1 = cand[base + 64 + lane]; bin1 = (c1.y >> SH) & (NBINS - 1); }
-                int r0 = 0, r1 = 0, run = 0;
-                static_for<NBINS>([&](auto Yc) {
-                    constexpr int y = Yc;
-                    const uint64_t m0 = __ballot(bin0 == y), m1 = __ballot(bin1 == y);
-                    const int p0 = __popcll(m0);
-                    if (bin0 == y) r0 = run + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
-                    if (bin1 == y) r1 = run + p0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-                    run += p0 + __popcll(m1);
-                });
-                if (lane < cnt) cand[base + r0] = c0;
-                if (lane + 64 < cnt) cand[base + r1] = c1;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-            };
-#if MVS_TAB_PIXSORT
-            // by pixel (column, then row: LSD), which keeps the row-pair order
-            // the K-loop spans need and puts a pixel's candidates next to each
-            // other, so their table gathers share lines
-            pass(std::integral_constant<int, 0>{}, std::integral_constant<int, 16>{});
-            pass(std::integral_constant<int, 4>{}, std::integral_constant<int, 8>{});
-#else
-            pass(std::integral_constant<int, 5>{}, std::integral_constant<int, 4>{});   // row pair
-#endif
+            // one stable counting pass by the row pair (pk >> 5) & 3 (ballots
+            // + mbcnt, in the wave's own part of the list)
+            constexpr int SH = 5, NBINS = 4;
+            int2 e0 = make_int2(0, 0), e1 = make_int2(0, 0);
+            int bin0 = NBINS, bin1 = NBINS;
+            if (lane < cnt) { e0 = cand[base + lane]; bin0 = (e0.y >> SH) & (NBINS - 1); }
+            if (lane + 64 < cnt) { e1 = cand[base + 64 + lane]; bin1 = (e1.y >> SH) & (NBINS - 1); }
+            int r0 = 0, r1 = 0, run = 0;
+            static_for<NBINS>([&](auto Yc) {
+                constexpr int y = Yc;
+                const uint64_t m0 = __ballot(bin0 == y), m1 = __ballot(bin1 == y);
+                const int p0 = __popcll(m0);
+                if (bin0 == y) r0 = run + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+                if (bin1 == y) r1 = run + p0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+                run += p0 + __popcll(m1);
+            });
+            if (lane < cnt) cand[base + r0] = e0;
+            if (lane + 64 < cnt) cand[base + r1] = e1;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
         TSTAMP(ts2);
         // ---- 3. + 4. units of two M-blocks (32 consecutive sorted candidates) ----
@@ -604,36 +395,18 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 }
                 // row 0 of the wave: each candidate's table row, published for
                 // the epilogue's lanes; its own S_a and w_a from the tables
-                int sa_raw[NH], tixv[NH];
+                int sa_raw[NH];
                 double wa_raw[NH];
 #pragma unroll
-                for (int h = 0; h < NH; ++h) { sa_raw[h] = 0; wa_raw[h] = 0.0; tixv[h] = 0; }
-                if constexpr (TR) {
-                    // every lane: its candidate m's table row, S_a and w_a
+                for (int h = 0; h < NH; ++h) { sa_raw[h] = 0; wa_raw[h] = 0.0; }
+                if (kh == 0) {
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
-                        tixv[h] = tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
-                        sa_raw[h] = tsb[tixv[h] + Rv[h]];
-                        wa_raw[h] = tw[tixv[h] + Rv[h]];
-                    }
-                } else if (kh == 0) {
-#pragma unroll
-                    for (int h = 0; h < NH; ++h) {
-                        // LT: element of the pixel inside the staged tile rows
-                        const int tix = LT ? (rrel[h] * MVS_TILE_W + qrel[h]) * VP : tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
+                        const int tix = tix0 + (rrel[h] * sc.W + qrel[h]) * VP;
                         ti[16 * h + m].tix = tix;
-                        if constexpr (MVS_TAB_TIXV) s_tix[wave * 32 + 16 * h + m] = tix;
-                        if constexpr (!FAST || !MVS_TAB_D64) ti_set_R(ti[16 * h + m], valid[h] ? Rv[h] : -1);
-                        if constexpr (LT) {
-                            sa_raw[h] = ls_sb[tix + Rv[h]];
-                            wa_raw[h] = w_of(ls_d[tix + Rv[h]]);
-                        } else if constexpr (MVS_TAB_WHATIF & 32) {   // measurement only: no S_a, w_a gathers
-                            sa_raw[h] = tix & 7;
-                            wa_raw[h] = 1.0;
-                        } else {
-                            sa_raw[h] = tsb[tix + Rv[h]];
-                            wa_raw[h] = tw[tix + Rv[h]];
-                        }
+                        ti[16 * h + m].R = valid[h] ? Rv[h] : -1;
+                        sa_raw[h] = tsb[tix + Rv[h]];
+                        wa_raw[h] = tw[tix + Rv[h]];
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -641,57 +414,18 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 // the epilogue's table values, one candidate step ahead: lane
                 // (kh, m) needs candidate 4 kh + i's S_b and w_b of views 16 nb + m
                 double sacc[NH][4];
-                if constexpr (MVS_TAB_WHATIF & 8) {
-#pragma unroll
-                    for (int h = 0; h < NH; ++h) sacc[h][0] = sacc[h][1] = sacc[h][2] = sacc[h][3] = 0.0;
-                }
                 int sbv[2][NH][NBLK];
                 double wv[2][NH][NBLK];
-                float wfv[2][NH][NBLK];
-                // SPLIT: a step's passing lanes -- num, the binary64 w being
-                // gathered for them, the pass mask -- summed one step later
-                int numB[2][NH][NBLK];
-                double wB[2][NH][NBLK];
-                uint64_t PB[2][NH][NBLK];
-                int4 tq[NH];   // MVS_TAB_TIXV: candidates 4 kh + 0..3's table rows
                 auto fetch = [&](auto ic) {
                     constexpr int i = decltype(ic)::value;
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
-                        int tix;
-                        if constexpr (MVS_TAB_TIXV && !LT)
-                            tix = (i == 0 ? tq[h].x : i == 1 ? tq[h].y : i == 2 ? tq[h].z : tq[h].w) + m;
-                        else
-                            tix = ti[16 * h + 4 * kh + i].tix + m;
+                        const int tix = ti[16 * h + 4 * kh + i].tix + m;
 #pragma unroll
                         for (int nb = 0; nb < NBLK; ++nb) {
-                            if constexpr (LT) {
-                                sbv[i & 1][h][nb] = ls_sb[tix + 16 * nb];
-                                wv[i & 1][h][nb] = w_of(ls_d[tix + 16 * nb]);
-                            } else if constexpr (SPLIT) {
-                                sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
-                                wfv[i & 1][h][nb] = twf[tix + 16 * nb];
-                            } else {
-                                // MVS_TAB_WHATIF (measurement only, wrong results): bit 0
-                                // drops the w gathers, bit 1 the S_b gathers
-                                if constexpr (MVS_TAB_WHATIF & 2) sbv[i & 1][h][nb] = tix & 255;
-                                else sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
-                                if constexpr (MVS_TAB_WHATIF & 1) wv[i & 1][h][nb] = 1e-3 * (double)(tix & 1023);
-                                else wv[i & 1][h][nb] = tw[tix + 16 * nb];
-                            }
+                            sbv[i & 1][h][nb] = tsb[tix + 16 * nb];
+                            wv[i & 1][h][nb] = tw[tix + 16 * nb];
                         }
-                    }
-                };
-                // SPLIT: step ip's deferred sum (its w gathers were issued a step ago)
-                auto consume = [&](auto ic) {
-                    constexpr int ip = decltype(ic)::value;
-#pragma unroll
-                    for (int h = 0; h < NH; ++h) {
-                        double sa = 0.0;
-#pragma unroll
-                        for (int nb = 0; nb < NBLK; ++nb)
-                            sa = fma_f64_lanes(sa, numB[ip & 1][h][nb], wB[ip & 1][h][nb], PB[ip & 1][h][nb]);
-                        sacc[h][ip] = sa;
                     }
                 };
                 TSTAMP(tk0);
@@ -762,19 +496,14 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         for (int nb = 0; nb < NBLK; ++nb) {
                             const v4i B = {(int)bv[cs][nb].x, (int)bv[cs][nb].y, (int)bv[cs][nb].z, (int)bv[cs][nb].w};
 #pragma unroll
-                            for (int h = 0; h < NH; ++h) {
-                                if constexpr (TR)   // C[h][nb] = views x candidates
-                                    C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(B, A[h], C[h][nb], 0, 0, 0);
-                                else
-                                    C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[h], B, C[h][nb], 0, 0, 0);
-                            }
+                            for (int h = 0; h < NH; ++h)
+                                C[h][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[h], B, C[h][nb], 0, 0, 0);
                         }
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 };
                 using I = std::integral_constant<int, 0>;
-                if constexpr (MVS_TAB_WHATIF & 4) {   // measurement only: no K-loop
-                } else if (span <= KSK) {
+                if (span <= KSK) {
                     kpass(std::integral_constant<int, KSK>{}, std::integral_constant<int, 1>{},
                           std::integral_constant<int, KSK - 2>{}, min(s_lo, KS - KSK), 0);
                 } else if (span == KSK + 1) {
@@ -787,121 +516,9 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 }
                 TSTAMP(tk1);
                 TSTAMP_ADD(5, tk1 - tk0);
-                if constexpr (TR) {
-                    // lane (kh, m) holds C[h][nb][r] = block h's candidate m, view
-                    // 16 nb + 4 kh + r: its table entries are 4 consecutive S_b
-                    // (8 B) and w (32 B) of the candidate's pixel row
-                    const int vb = 4 * kh;
-                    uint2 sbq[NH][NBLK];
-                    double2 wq0[NH][NBLK], wq1[NH][NBLK];
-#pragma unroll
-                    for (int h = 0; h < NH; ++h)
-#pragma unroll
-                        for (int nb = 0; nb < NBLK; ++nb) {
-                            const int o = tixv[h] + 16 * nb + vb;
-                            sbq[h][nb] = *(const uint2*)(tsb + o);
-                            wq0[h][nb] = *(const double2*)(tw + o);
-                            wq1[h][nb] = *(const double2*)(tw + o + 2);
-                        }
-                    const int jl = lane & 31;   // permlane swaps: partner = lane ^ 16, ^ 32
-#pragma unroll
-                    for (int h = 0; h < NH; ++h) {
-                        const double wa = wa_raw[h];
-                        const float T = valid[h] ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf("");
-                        const float gT = 2e-6f * fabsf(T);
-                        const int Sa = -sa_raw[h];
-                        uint32_t m12 = 0u;
-                        double sum = 0.0;
-                        float mn = __builtin_inff();
-                        // views in descending order: bit 4 nb + r of m12 = view (nb, r)
-                        static_for<NBLK * 4>([&](auto Qc) {
-                            constexpr int q = NBLK * 4 - 1 - (int)Qc;
-                            constexpr int nb = q >> 2, r = q & 3;
-                            const uint32_t wd = (r < 2) ? sbq[h][nb].x : sbq[h][nb].y;
-                            const int sb = (r & 1) ? ((int)wd >> 16) : (int)(int16_t)(wd & 0xffffu);
-                            const int num = __mul24(Sa, sb) + __mul24(NPX, C[h][nb][r]);
-                            const double w = r == 0 ? wq0[h][nb].x : r == 1 ? wq0[h][nb].y : r == 2 ? wq1[h][nb].x : wq1[h][nb].y;
-                            // ncc > thr <=> num w_b > T (module comment); a constant
-                            // window (w_b nan) never passes
-                            const float x = fmaf((float)num, (float)w, -T);
-                            const uint64_t P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);      // ogt
-                            m12 = m12 + m12 + (x > 0.0f ? 1u : 0u);
-                            sum = fma_f64_lanes(sum, num, w, P);
-                            mn = fminf(mn, fabsf(x));
-                        });
-                        // the lane's bits into the candidate's mask words
-                        uint32_t mw[2] = {0u, 0u};
-#pragma unroll
-                        for (int nb = 0; nb < NBLK; ++nb) mw[nb >> 1] |= ((m12 >> (4 * nb)) & 15u) << (16 * (nb & 1) + vb);
-                        // combine the four lanes of candidate m (kh = 0..3)
-                        auto swap_or = [&](uint32_t x) {
-                            auto r16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-                            x = r16[0] | r16[1];
-                            auto r32 = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-                            return r32[0] | r32[1];
-                        };
-                        auto swap_add = [&](double v) {
-                            const unsigned long long u = __double_as_longlong(v);
-                            auto l16 = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
-                            auto h16 = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
-                            // the partner's half is the element that differs from this lane's own
-                            const bool lo16 = (jl & 16) == 0;
-                            const double p16 = __longlong_as_double(((unsigned long long)(lo16 ? h16[1] : h16[0]) << 32) |
-                                                                    (lo16 ? l16[1] : l16[0]));
-                            v += p16;
-                            const unsigned long long u2 = __double_as_longlong(v);
-                            auto l32 = __builtin_amdgcn_permlane32_swap((uint32_t)u2, (uint32_t)u2, false, false);
-                            auto h32 = __builtin_amdgcn_permlane32_swap((uint32_t)(u2 >> 32), (uint32_t)(u2 >> 32), false, false);
-                            const bool lo32 = lane < 32;
-                            const double p32 = __longlong_as_double(((unsigned long long)(lo32 ? h32[1] : h32[0]) << 32) |
-                                                                    (lo32 ? l32[1] : l32[0]));
-                            return v + p32;
-                        };
-                        auto swap_min = [&](float v) {
-                            auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-                            v = fminf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
-                            auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-                            return fminf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
-                        };
-                        mw[0] = swap_or(mw[0]);
-                        if constexpr (NBLK > 2) mw[1] = swap_or(mw[1]);
-                        const double mine = a.avg != nullptr ? swap_add(sum) : 0.0;
-                        const bool gg = swap_min(mn) < gT;
-                        if (kh == 0 && valid[h]) {
-                            uint64_t mk = (uint64_t)mw[0] | ((uint64_t)mw[1] << 32);
-                            // the reference view itself is no V entry (MVS2.py:66-67)
-                            const uint64_t self = (mk >> Rv[h]) & 1ull;
-                            mk &= ~(1ull << Rv[h]);
-                            const int cnt = __popcll(mk);
-                            const int64_t idx = e[h].x;
-                            double av = 0.0;
-                            if (a.avg) {
-                                // its own term num_RR w_a = D_a w_a = 1 / w_a leaves the sum
-                                double inv = __builtin_amdgcn_rcp(wa);
-                                inv = inv * (2.0 - wa * inv);
-                                const double sm = self ? mine - inv : mine;
-                                av = cnt ? sm * (kn * wa) * s_recip[cnt] : 0.0;
-                            }
-                            if (a.rec) {
-                                const unsigned long long ab = __double_as_longlong(av);
-                                *(uint4*)(a.mask + 2 * idx) = make_uint4((uint32_t)mk, (uint32_t)(mk >> 32), (uint32_t)ab,
-                                                                         (uint32_t)(ab >> 32));
-                            } else {
-                                a.mask[idx] = mk;
-                                a.count[idx] = cnt;
-                                if (a.avg) a.avg[idx] = av;
-                            }
-                            if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
-                        }
-                    }
-                } else {
                 // the first candidate step's table values (issued after the K-loop:
                 // in flight across it they would hold 18 registers)
-                if constexpr (MVS_TAB_TIXV && !LT) {
-#pragma unroll
-                    for (int h = 0; h < NH; ++h) tq[h] = *(const int4*)(s_tix + wave * 32 + 16 * h + 4 * kh);
-                }
-                if constexpr (!(MVS_TAB_WHATIF & 8)) fetch(std::integral_constant<int, 0>{});
+                fetch(std::integral_constant<int, 0>{});
                 // the candidates' decision constants (row 0), now that S_a, w_a are in
                 double my_wa[NH];
 #pragma unroll
@@ -911,15 +528,11 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                     for (int h = 0; h < NH; ++h) {
                         const double wa = wa_raw[h];
                         ti[16 * h + m].Sa = -sa_raw[h];
-                        // FAST: T = thr (n-1)/n sqrt(da) (binary32: a 1-ulp reciprocal;
-                        // binary64: a correctly rounded quotient; both well inside the
-                        // guard band); else the decision is on ncc
-#if MVS_TAB_D64
-                        if constexpr (FAST) ti[16 * h + m].T = valid[h] ? tqd / wa : __builtin_nan("");
-#else
+                        // FAST: T = thr (n-1)/n sqrt(da) (binary32: a 1-ulp
+                        // reciprocal, well inside the guard band); else the
+                        // decision is on ncc
                         ti[16 * h + m].T = FAST ? (valid[h] ? tqf * __builtin_amdgcn_rcpf((float)wa) : __builtin_nanf(""))
                                                 : 0.0f;
-#endif
                         my_wa[h] = wa;
                     }
                 }
@@ -929,31 +542,17 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                 uint32_t pmv[NH], gdv[NH];
 #pragma unroll
                 for (int h = 0; h < NH; ++h) pmv[h] = gdv[h] = 0u;
-                if constexpr (MVS_TAB_WHATIF & 8) {   // keep the window products alive (outputs untouched)
-                    int sc_ = 0;
-#pragma unroll
-                    for (int h = 0; h < NH; ++h)
-#pragma unroll
-                        for (int nb = 0; nb < NBLK; ++nb) sc_ += C[h][nb][0] + C[h][nb][1] + C[h][nb][2] + C[h][nb][3];
-                    if (sc_ == 0x7fffffff && a.exact_hits) atomicAdd(a.exact_hits, 1);
-                }
-                if constexpr (!(MVS_TAB_WHATIF & 8))   // measurement only: no decisions
                 static_for<4>([&](auto Ic) {
                     constexpr int i = Ic;
                     if constexpr (i < 3) fetch(std::integral_constant<int, i + 1>{});
 #pragma unroll
                     for (int h = 0; h < NH; ++h) {
                         const TabInfo c = ti[16 * h + 4 * kh + i];
-#if MVS_TAB_D64
-                        const double gT = 2e-6 * fabs(c.T);
-                        double ax[NBLK];
-#else
                         const float gT = 2e-6f * fabsf(c.T);
                         float ax[NBLK];
-#endif
                         double ca = 0.0;
-                        const int cR = ti_R(c);
-                        if constexpr (!FAST) ca = cR < 0 ? 0.0 : kn * (LT ? w_of(ls_d[c.tix + cR]) : tw[c.tix + cR]);
+                        const int cR = c.R;
+                        if constexpr (!FAST) ca = cR < 0 ? 0.0 : kn * tw[c.tix + cR];
                         double sa = 0.0;
                         uint64_t g = 0;
                         static_for<NBLK>([&](auto Nc) {
@@ -961,35 +560,16 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                             const int vl = 16 * nb + m;
                             const int num = __mul24(c.Sa, sbv[i & 1][h][nb]) + __mul24(NPX, C[h][nb][i]);
                             uint64_t P;
-                            if constexpr (SPLIT) {
-                                // the same binary32 decision ((float)w is the wf entry)
-                                const float x = fmaf((float)num, wfv[i & 1][h][nb], -c.T);
-                                P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
-                                ax[nb] = x;
-                                numB[i & 1][h][nb] = num;
-                                PB[i & 1][h][nb] = P;
-                                double wb;   // lanes that do not pass never read it
-                                if (x > 0.0f) wb = tw[c.tix + m + 16 * nb];   // passing lanes only
-                                wB[i & 1][h][nb] = wb;
-                            } else if constexpr (FAST) {
+                            if constexpr (FAST) {
                                 const double w = wv[i & 1][h][nb];
                                 // ncc > thr <=> num w_b > T; a constant window (w_b nan)
                                 // never passes.  The candidate's own view R passes (its ncc
                                 // is n/(n-1) > thr): its mask bit and its term of the sum
                                 // are taken out once per candidate
-#if MVS_TAB_D64
-                                const double numd = (double)num;
-                                const double x = fma(numd, w, -c.T);
-                                P = __builtin_amdgcn_fcmp(x, 0.0, 2);                           // ogt
-                                ax[nb] = x;
-                                if constexpr (MVS_TAB_MAXSUM) sa += fmax(x, 0.0);   // a nan x adds 0
-                                else sa = fma_f64_lanes_d(sa, numd, w, P);
-#else
                                 const float x = fmaf((float)num, (float)w, -c.T);
                                 P = __builtin_amdgcn_fcmpf(x, 0.0f, 2);                         // ogt
                                 ax[nb] = x;
                                 sa = fma_f64_lanes(sa, num, w, P);
-#endif
                             } else {
                                 const double w = wv[i & 1][h][nb];
                                 const double ncc = (double)num * w * ca;
@@ -1002,26 +582,16 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                             pmv[h] = writelane<2 * (i * NBLK + nb) + 1>(pmv[h], (uint32_t)(P >> 32));
                         });
                         if constexpr (FAST) {
-#if MVS_TAB_D64
-                            double mn = fabs(ax[0]);
-#pragma unroll
-                            for (int nb = 1; nb < NBLK; ++nb) mn = fmin(mn, fabs(ax[nb]));
-                            g = __builtin_amdgcn_fcmp(mn, gT, 4);                                // olt
-#else
                             float mn = fabsf(ax[0]);
 #pragma unroll
                             for (int nb = 1; nb < NBLK; ++nb) mn = fminf(mn, fabsf(ax[nb]));
                             g = __builtin_amdgcn_fcmpf(mn, gT, 4);                               // olt
-#endif
                         }
                         gdv[h] = writelane<2 * i>(gdv[h], (uint32_t)g);
                         gdv[h] = writelane<2 * i + 1>(gdv[h], (uint32_t)(g >> 32));
-                        if constexpr (!SPLIT) sacc[h][i] = sa;
+                        sacc[h][i] = sa;
                     }
-                    // the previous step's sum: its gathers had this step's decisions to land
-                    if constexpr (SPLIT && i > 0) consume(std::integral_constant<int, i - 1>{});
                 });
-                if constexpr (SPLIT) consume(std::integral_constant<int, 3>{});
                 // owner lane c = 4 j + i (row 0) of each block's candidate c: its mask
                 // bits, guard bits and sum from the lanes that hold them
                 const int jj = m >> 2, ii = m & 3;
@@ -1052,18 +622,12 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         const int64_t idx = e[h].x;
                         double av = 0.0;
                         if (a.avg) {
-#if MVS_TAB_D64 && MVS_TAB_MAXSUM
-                            // the passing terms' T (see MVS_TAB_MAXSUM)
-                            if constexpr (FAST) mine += (double)(cnt + (int)self) * ti[16 * h + m].T;
-#endif
                             // its own term num_RR w_a = D_a w_a = 1 / w_a leaves the sum
                             double inv = __builtin_amdgcn_rcp(my_wa[h]);
                             inv = inv * (2.0 - my_wa[h] * inv);
                             const double sum = self ? mine - inv : mine;
                             av = cnt ? sum * (kn * my_wa[h]) * s_recip[cnt] : 0.0;
                         }
-                        if constexpr (MVS_TAB_WHATIF & 64) {   // measurement only: no output stores
-                        } else
                         if (a.rec) {
                             // one 16-B record [mask word, avg] (|V| = popcount)
                             const unsigned long long ab = __double_as_longlong(av);
@@ -1077,26 +641,17 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
                         if (gg) t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)idx, dcur.x, e[h].y, 0);
                     }
                 }
-                }
                 TSTAMP(tk2);
                 TSTAMP_ADD(6, tk2 - tk1);
             };
             if (nh == 2) unit(std::integral_constant<int, 2>{});
             else unit(std::integral_constant<int, 1>{});
             TSTAMP_ADD(4, nh);
-            if constexpr (DB && MVS_TAB_DMA_LATE) {
-                if (fb == b0 && nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
-            }
-            if constexpr (MVS_TAB_SHALLOW && MVS_TAB_LATE_CLAIM == 1) {
-                if (fb == b0 && tid == 0 && nx1 < n_units) pend = claim();
-            }
+            // thread 0 claims item k+2 after wave 0's first unit: less held
+            // back when the queue runs dry
+            if (fb == b0 && tid == 0 && nx1 < n_units) pend = claim();
         }
-        if constexpr (MVS_TAB_SHALLOW && MVS_TAB_LATE_CLAIM) {
-            if ((MVS_TAB_LATE_CLAIM == 2 || b0 >= b1) && tid == 0 && nx1 < n_units) pend = claim();
-        }
-        if constexpr (DB && MVS_TAB_DMA_LATE) {
-            if (b0 >= b1 && nx1 < n_units) stage(dst1, std::integral_constant<int, buf ^ 1>{});
-        }
+        if (b0 >= b1 && tid == 0 && nx1 < n_units) pend = claim();
         TSTAMP(ts3);
         if (wave == 0) TSTAMP_ADD(0, 1);
         TSTAMP_ADD(1, ts1 - ts0);
@@ -1110,11 +665,6 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         }
         cur = nx1;
         dcur = desc(it1, c1);
-        hcur = __builtin_amdgcn_readfirstlane(it1.y >> 20);
-#if !MVS_TAB_SHALLOW
-        nx1 = nx2;
-        it1 = make_int2(__builtin_amdgcn_readfirstlane(it2.x), __builtin_amdgcn_readfirstlane(it2.y));
-#endif
         return true;
     };
     for (;;) {
@@ -1134,6 +684,7 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
     }
 #endif
 }
+
 
 // hipFuncAttributeMaxDynamicSharedMemorySize is not needed: all LDS is static
 template <int WID, int NBLK>

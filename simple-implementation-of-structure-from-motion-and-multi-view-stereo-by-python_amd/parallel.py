@@ -20,62 +20,138 @@ no communication while scoring.  Two exchanges:
   (8 B per child at V <= 64) are all-gathered; every rank then runs the
   identical ordered commit (mvs_stage_* in include/mvs_amd.h).
 """
+import atexit
+import ctypes
+import os
+import weakref
+
 import numpy as np
 import torch
 import torch.distributed as dist
 
 
+class MaskedStream:
+    """Owner of a stream of `device` whose kernels run on all CUs but
+    `free_cus` of them (hipExtStreamCreateWithCUMask; bit k of the mask = CU
+    k as HIP numbers them, the highest free_cus left out), or with
+    complement=True on those free_cus CUs only.  `.stream` is the torch
+    ExternalStream, `.cus` the CUs in its mask.  The multi-GPU step's `mask`
+    layout scores on the first kind, with the scorer's grid at two workgroups
+    per CU of the mask (MvsContext.set_scorer_grid), and packs on the second
+    (PointsExchange) -- DESIGN.md section 7.
+
+    close() (or the with-block's end, or garbage collection) waits for the
+    stream, tells every live MvsContext that it retires (their lazy
+    cross-stream ordering must not record an event on it later), then
+    destroys it.  Streams still open at interpreter exit are closed by an
+    atexit hook, before the HIP runtime and a profiler's tool library tear
+    down: a masked stream left to the runtime's own static destructors ended
+    a rocprofv3 run in a SIGSEGV inside __cxa_finalize (profiles/r05/,
+    DESIGN.md 7)."""
+
+    _live = weakref.WeakSet()
+
+    def __init__(self, device, free_cus, complement=False):
+        dev = torch.device(device)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        free = min(max(int(free_cus), 1), ncu - 1)
+        lo, hi = (ncu - free, ncu) if complement else (0, ncu - free)
+        words = []
+        for w in range((ncu + 31) // 32):
+            v = 0
+            for b in range(32):
+                if lo <= 32 * w + b < hi:
+                    v |= 1 << b
+            words.append(v)
+        arr = (ctypes.c_uint32 * len(words))(*words)
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            rc = _hip().hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), arr)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+        self._handle = handle.value
+        self.device = dev
+        self.cus = hi - lo
+        self.stream = torch.cuda.ExternalStream(handle.value, device=dev)
+        MaskedStream._live.add(self)
+
+    @property
+    def cuda_stream(self):
+        return self._handle
+
+    def close(self):
+        h, self._handle = getattr(self, "_handle", None), None
+        if not h:
+            return
+        MaskedStream._live.discard(self)
+        self.stream.synchronize()
+        from . import _lib
+        _lib.stream_retiring(h)
+        rc = _hip().hipStreamDestroy(ctypes.c_void_p(h))
+        if rc != 0:
+            raise RuntimeError(f"hipStreamDestroy failed ({rc})")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@atexit.register
+def _close_masked_streams():
+    # registered after _lib's context hook (this module imports later), so
+    # it runs first: streams retire while their contexts are still open
+    for ms in list(MaskedStream._live):
+        try:
+            ms.close()
+        except Exception:
+            pass
+
+
 def cu_masked_stream(device, free_cus, complement=False):
-    """A stream of `device` whose kernels run on all CUs but `free_cus` of
-    them (hipExtStreamCreateWithCUMask; bit k of the mask = CU k as HIP
-    numbers them, the highest free_cus left out), or with complement=True
-    on those free_cus CUs only; as (torch ExternalStream, CUs in its mask).
-    The multi-GPU step scores on the first kind, with the scorer's grid at
-    two workgroups per CU of the mask (MvsContext.set_scorer_grid), and
-    packs its accepted points on the second (PointsExchange): the exchange
-    then never takes CUs from the next sweep's kernels.
-    Release it with destroy_stream()."""
-    import ctypes
-    dev = torch.device(device)
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    free = min(max(int(free_cus), 1), ncu - 1)
-    lo, hi = (ncu - free, ncu) if complement else (0, ncu - free)
-    words = []
-    for w in range((ncu + 31) // 32):
-        v = 0
-        for b in range(32):
-            if lo <= 32 * w + b < hi:
-                v |= 1 << b
-        words.append(v)
-    arr = (ctypes.c_uint32 * len(words))(*words)
-    handle = ctypes.c_void_p()
-    with torch.cuda.device(dev):
-        rc = _hip().hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), arr)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    return torch.cuda.ExternalStream(handle.value, device=dev), hi - lo
+    """A MaskedStream (see there); release it with close() or destroy_stream()."""
+    return MaskedStream(device, free_cus, complement)
 
 
 def destroy_stream(stream):
-    """Release a stream of cu_masked_stream (after its work has completed)."""
-    stream.synchronize()
-    _hip().hipStreamDestroy(ctypes_void_p(stream.cuda_stream))
-
-
-def ctypes_void_p(x):
-    import ctypes
-    return ctypes.c_void_p(x)
+    """Release a MaskedStream (after its work has completed)."""
+    if not isinstance(stream, MaskedStream):
+        raise TypeError("destroy_stream takes a MaskedStream (cu_masked_stream)")
+    stream.close()
 
 
 _HIP = None
 
 
 def _hip():
-    """The HIP runtime torch loaded (its libamdhip64)."""
+    """The HIP runtime this process already runs (the libamdhip64 that torch
+    loaded), opened without loading anything: a second copy of the runtime
+    would hand out streams that torch and libmvs_amd do not know."""
     global _HIP
     if _HIP is None:
-        import ctypes
-        _HIP = ctypes.CDLL("libamdhip64.so")
+        path = None
+        with open("/proc/self/maps") as f:
+            for ln in f:
+                p = ln.split()[-1] if len(ln.split()) >= 6 else ""
+                if os.path.basename(p).startswith("libamdhip64.so"):
+                    path = p
+                    break
+        if path is None:
+            raise RuntimeError("the HIP runtime (libamdhip64) is not loaded in this process; import torch first")
+        try:
+            _HIP = ctypes.CDLL(path, mode=os.RTLD_NOLOAD)
+        except OSError as e:
+            raise RuntimeError(f"cannot open the loaded HIP runtime {path}: {e}") from e
+        _HIP.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                      ctypes.POINTER(ctypes.c_uint32)]
+        _HIP.hipStreamDestroy.argtypes = [ctypes.c_void_p]
     return _HIP
 
 
@@ -147,8 +223,11 @@ class PointsExchange:
         self.send = [torch.zeros((self.cap + 1, self.width), dtype=torch.int64, device=device) for _ in range(2)]
         self.recv = [torch.zeros((self.world * (self.cap + 1), self.width), dtype=torch.int64, device=device)
                      for _ in range(2)]
-        # comm_stream: e.g. a cu_masked_stream(complement=True) of the CUs the
-        # scoring stream leaves out
+        # comm_stream: e.g. a MaskedStream(complement=True) of the CUs the
+        # scoring stream leaves out (held here, so that it outlives the exchange)
+        self._comm_owner = comm_stream if isinstance(comm_stream, MaskedStream) else None
+        if self._comm_owner is not None:
+            comm_stream = self._comm_owner.stream
         self.comm = comm_stream if comm_stream is not None else (
             torch.cuda.Stream(self.device) if cuda and (self.world > 1 or self.pack_on_comm) else None)
         self.done = [None, None]
@@ -173,6 +252,11 @@ class PointsExchange:
                 scored = torch.cuda.Event()
                 scored.record(cur)
                 self.comm.wait_event(scored)          # send[b]'s last gather ran on comm itself
+                # the pack reads the slice's outputs on the comm stream: the
+                # caching allocator must not hand them out before it has run
+                for t_ in (count, mask, cc):
+                    if t_ is not None:
+                        t_.record_stream(self.comm)
                 self.ctx.pack_accepted(offset, count, mask, vlb, self.send[b], stream=self.comm.cuda_stream, c=cc)
                 rd = torch.cuda.Event()
                 rd.record(self.comm)
