@@ -72,19 +72,54 @@ def logical_bytes(V, wid):
     return V * (2 * wid + 1) ** 2 + 32 + 8 * ((V + 63) // 64) + 16
 
 
-def floor_bytes(V, H, W, n):
-    """The unique bytes one scorer launch must move between HBM and the
-    chip: the scene's moment tables (S_b int16 + w binary64 per (pixel,
-    view) at V <= 64, S_b int16 + D int32 at V > 64; (H W + 16) VP entries),
-    the view-major gray copy gv (V H Wp bytes, Wp = 16-aligned W + 32), the
-    bucket entries read (8 B per candidate) and the records written
-    (8 (ceil(V/64) + 1) B per candidate)."""
+def floor_bytes(rgb, xy, ref, wid, n):
+    """The unique bytes one scorer launch must move between HBM and the chip,
+    from the sweep itself: the candidates the scorer sees are those with a
+    valid window whose reference window is not constant (k_bin settles the
+    rest), and for them it must read the moment-table rows of their distinct
+    pixels (S_b int16 + w binary64 per view at V <= 64, S_b + D int32 at
+    V > 64; VP views per row), the gv regions of their distinct tiles (V views
+    x (8 + 2 wid) rows x 32 B), their bucket entries (8 B) and write their
+    records (8 (ceil(V/64) + 1) B).  rgb: (V, H, W, 3) uint8 (host or device); xy, ref:
+    device tensors of the sweep.  The windows' constancy is recomputed here
+    from integral images of the gray stack (OpenCV's BGR2GRAY weights on the
+    RGB data, HarrisFeatures.py:125)."""
+    import torch
+    V, H, W = rgb.shape[0], rgb.shape[1], rgb.shape[2]
     words = (V + 63) // 64
     vp = 64 * words if V > 64 else 16 * ((V + 15) // 16)
-    tables = (H * W + 16) * vp * (6 if V > 64 else 10)
-    wp = (W + 15) // 16 * 16 + 32
-    parts = {"tables": tables, "gv": V * H * wp, "bucket_entries": 8 * n, "records": 8 * (words + 1) * n}
-    return sum(parts.values()), parts
+    npx = (2 * wid + 1) ** 2
+    q = xy[:, 0].trunc().long()
+    r = xy[:, 1].trunc().long()
+    ok = (r - wid >= 0) & (r + wid + 1 < H) & (q - wid > 0) & (q + wid + 1 < W)
+    q, r, R = q[ok], r[ok], ref[ok].long()
+    S = torch.zeros(len(q), dtype=torch.int64, device=xy.device)
+    Q = torch.zeros_like(S)
+    for v0 in range(0, V, 16):   # the integral images 16 views at a time (bounded memory)
+        v1 = min(V, v0 + 16)
+        c = torch.as_tensor(np.ascontiguousarray(rgb[v0:v1]) if isinstance(rgb, np.ndarray) else rgb[v0:v1])
+        c = c.to(xy.device).int()
+        g = ((c[..., 0] * 1868 + c[..., 1] * 9617 + c[..., 2] * 4899 + 8192) >> 14).long()
+        del c
+        sel = (R >= v0) & (R < v1)
+        for src, dst in ((g, S), (g * g, Q)):
+            ii = torch.zeros((v1 - v0, H + 1, W + 1), dtype=torch.int64, device=xy.device)
+            ii[:, 1:, 1:] = src.cumsum(1).cumsum(2)
+            rv, rr, qq = R[sel] - v0, r[sel], q[sel]
+            dst[sel] = (ii[rv, rr + wid + 1, qq + wid + 1] - ii[rv, rr - wid, qq + wid + 1]
+                        - ii[rv, rr + wid + 1, qq - wid] + ii[rv, rr - wid, qq - wid])
+            del ii
+        del g
+    seen = npx * Q != S * S
+    q, r = q[seen], r[seen]
+    binned = int(seen.sum())
+    pixels = int(torch.unique(r * W + q).numel())
+    ntx = (W + 15) // 16
+    tiles = int(torch.unique((r // 8) * ntx + q // 16).numel())
+    parts = {"tables": pixels * vp * (6 if V > 64 else 10), "gv": tiles * V * (8 + 2 * wid) * 32,
+             "bucket_entries": 8 * binned, "records": 8 * (words + 1) * binned}
+    return sum(parts.values()), parts, {"scored_candidates": binned, "of": n, "distinct_pixels": pixels,
+                                        "tiles": tiles}
 
 
 def score(cx, sw, wid, thr, stream, rec=None):
@@ -166,7 +201,7 @@ def direct_path(before, after):
             "numpy_order_ncc_per_sweep": (after["exact"] - before["exact"]) / b, "sweeps": b}
 
 
-def roofline(entry, V, H, W, wid, n, kms, kernel):
+def roofline(entry, V, wid, n, kms, kernel, floor):
     """Roofs of the dominant kernel: measured HBM bytes, VALU-busy cycles and
     MFMA i8 operations per launch (PMC) over the live launch time.  The binding
     roof is the one with the largest fraction; each frac <= 1 because a unit
@@ -174,10 +209,10 @@ def roofline(entry, V, H, W, wid, n, kms, kernel):
     launch (floor_bytes): useful_frac = floor / launch time / 8 TB/s, and
     traffic / floor = how much of the counted traffic is re-reads."""
     npx = (2 * wid + 1) ** 2
-    fb, fparts = floor_bytes(V, H, W, n)
+    fb, fparts, fset = floor
     out = {"kernel": entry["kernel"] if entry else kernel, "kernel_ms": kms,
            "candidates_per_launch": n,
-           "floor_bytes": fb, "floor_parts": fparts,
+           "floor_bytes": fb, "floor_parts": fparts, "floor_set": fset,
            "useful_GBps": fb / (kms * 1e-3) / 1e9,
            "useful_frac": fb / (kms * 1e-3) / PEAK_HBM,
            "survey_model_bytes_per_candidate": logical_bytes(V, wid),
@@ -639,7 +674,8 @@ def main():
         "direct_path": direct,
         "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream, a.thr, a.wid),
     }
-    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, H, W, a.wid, n, kms, kernel_name)
+    out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms, kernel_name,
+                               floor_bytes(rgb, sw["xy"], sw["ref"], a.wid, n))
     if solo and not a.no_overlap:
         # the multi-GPU layout: scoring on the CU-masked stream, the pack and
         # the proxy of RCCL's all-gather on the CUs it leaves out
@@ -674,7 +710,8 @@ def main():
             out["secondary"] = {"wid": a.secondary_wid, "value": n * s2 / dt2, "kernel_ms": kms2,
                                 "score_call_ms": pms2, "direct_path": direct_path(st0, scorer_stats(ctx)),
                                 "roofline": roofline(pmc_entry(a.scene, V, a.secondary_wid, n, kernel_name), V,
-                                                     H, W, a.secondary_wid, n, kms2, kernel_name)}
+                                                     a.secondary_wid, n, kms2, kernel_name,
+                                                     floor_bytes(rgb, sw["xy"], sw["ref"], a.secondary_wid, n))}
 
     if solo and a.scene == "dino" and not a.no_stage:
         sd = dict(np.load(os.path.join(REPO, "tests", "golden", "seeds_dino.npz")))
@@ -702,7 +739,6 @@ def main():
         rrgb, rK, rR, rt = make_scene("ring256")
         rV, rH, rW = rrgb.shape[:3]
         rctx = pkg.MvsContext(rrgb, rK, rR, rt, device=local)
-        del rrgb
         rsw = sweep_inputs(rV, rK, rR, rt, rW, rH, a.n, False)
         s3 = max(a.steps // 5, 5)
         rdt, rkms, rpms, _ = timed(rctx, rsw, a.wid, s3, 2, exchange=False)
@@ -711,9 +747,11 @@ def main():
                           "value": rsw["n"] * s3 / rdt, "unit": "candidates/s", "kernel": rctx.timed_kernel(),
                           "kernel_ms": rkms, "score_call_ms": rpms,
                           "accepted_per_sweep": int((host_outputs(rsw)[1] >= 3).sum()),
-                          "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"], rctx.timed_kernel()), rV, rH,
-                                               rW, a.wid, rsw["n"], rkms, rctx.timed_kernel())}
+                          "roofline": roofline(pmc_entry("ring256", rV, a.wid, rsw["n"], rctx.timed_kernel()), rV,
+                                               a.wid, rsw["n"], rkms, rctx.timed_kernel(),
+                                               floor_bytes(rrgb, rsw["xy"], rsw["ref"], a.wid, rsw["n"]))}
         rctx.close()
+        del rrgb
 
     if solo and not a.no_cpu_baseline:
         from oracle import oracle as orc

@@ -157,7 +157,7 @@ int mvs_kernel_timing(mvs_ctx* ctx, int enable);
 int mvs_kernel_time(mvs_ctx* ctx, double* total_ms, int64_t* launches);
 const char* mvs_timed_kernel(const mvs_ctx* ctx);
 /* Number of per-view NCC decisions that fell inside the direct scorer's guard
- * band around the threshold (relative 1e-8 on the squared comparison; 1e-9
+ * band around the threshold (relative 1e-11 on the squared comparison; 1e-9
  * absolute when min_ncc < 0.01) and were re-evaluated in numpy order since the
  * context was created.  (The tiled scorer's own band, 2e-6 relative on its
  * binary32 comparison, sends a candidate to the direct scorer.) */

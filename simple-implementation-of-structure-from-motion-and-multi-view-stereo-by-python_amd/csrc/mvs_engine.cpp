@@ -330,6 +330,7 @@ struct mvs_ctx {
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
     DevBuf<double> mom_w[MVS_MAX_WID + 1];     // V <= 64
     DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V > 64 (moments_dtab)
+    DevBuf<uint16_t> mom_flat[MVS_MAX_WID + 1];   // constant-window bits (MomentsDev.flat)
     bool mom_ok[MVS_MAX_WID + 1] = {};
     int moments_vp() const { return V > MVS_GROUP_VIEWS ? 64 * ((V + 63) / 64) : 16 * ((V + 15) / 16); }
     MomentsDev moments(int wid) const {
@@ -337,6 +338,7 @@ struct mvs_ctx {
         m.sb = mom_sb[wid].p;
         m.w = mom_w[wid].p;
         m.d = mom_d[wid].p;
+        m.flat = mom_flat[wid].p;
         m.VP = moments_vp();
         m.wid = wid;
         return m;
@@ -361,14 +363,17 @@ struct mvs_ctx {
                 mom_sb[wid].alloc((size_t)elems);
                 if (moments_dtab(V)) mom_d[wid].alloc((size_t)elems);
                 else mom_w[wid].alloc((size_t)elems);
+                mom_flat[wid].alloc((size_t)(elems / 16));
             } catch (const Fail&) {
                 mom_sb[wid].release();
                 mom_d[wid].release();
                 mom_w[wid].release();
+                mom_flat[wid].release();
                 (void)hipGetLastError();   // the failed hipMalloc's error is not this call's
                 return false;
             }
             HIPCHK(hipMemsetAsync(mom_sb[wid].p, 0, (size_t)elems * sizeof(int16_t), s));
+            HIPCHK(hipMemsetAsync(mom_flat[wid].p, 0, (size_t)(elems / 16) * sizeof(uint16_t), s));
             if (moments_dtab(V))
                 HIPCHK(hipMemsetAsync(mom_d[wid].p, 0, (size_t)elems * sizeof(int32_t), s));
             else

@@ -143,6 +143,11 @@ struct MomentsDev {
     int16_t* sb;
     double* w;      // V <= 64
     int32_t* d;     // moments_dtab(V): V > 64
+    // bit (v & 15) of flat[(y * W + x) * (VP / 16) + v / 16]: view v's window
+    // at (x, y) is constant (D = 0) -- 2 B per pixel and 16 views, L2-sized
+    // (1.8 MB at dinoRing): k_bin settles candidates with a constant
+    // reference window from it
+    uint16_t* flat;
     int VP;
     int wid;
 };

@@ -120,7 +120,13 @@ DEV double wave_sum(double x) {
 // o = (q - WID) & 3.  Lane 0 of the wave writes mask/count/avg.
 // Decision without sqrt/div: for thr >= 0.01, ncc > thr  <=>  L > 0 and
 // L^2 > thr^2 (n-1)^2 da db  with L = n*num (exact in binary64); a relative band
-// of 1e-8 around it goes to the numpy-order path.
+// of 1e-11 around it (5e-12 relative on the NCC) goes to the numpy-order
+// path.  The comparison itself is exact to ~6e-16 relative (L is an exact
+// integer, rhs three roundings); the reference's numpy-order NCC differs from
+// the exact value by < 1e-14 relative (121 terms, std from pairwise sums), so
+// the band covers every pair whose reference decision could differ from the
+// exact one with a margin of ~500.  (It was 1e-8: 104 numpy-order
+// evaluations per wid-3 sweep then, most of k_score_fix's 26 us.)
 template <int WID, int NS, class Fetch>
 DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fetch&& fetch,
                          uint64_t* mask_out, int32_t* count_out, double* avg_out, int32_t* exact_hits) {
@@ -205,7 +211,7 @@ DEV void wave_score_core(const SceneDev& sc, int R, int q, int r, double thr, Fe
                     const double tk = thr * (double)(NPX - 1);
                     const double rhs = (tk * tk) * ((double)da * (double)db);
                     const double diff = L * L - rhs;
-                    if (fabs(diff) <= 1e-8 * rhs) {
+                    if (fabs(diff) <= 1e-11 * rhs) {
                         ncc = exact_ncc_stack<WID>(sc, R, v, q, r);
                         atomicAdd(exact_hits, 1);
                         pass = ncc > thr;
@@ -483,19 +489,17 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     // a candidate whose reference window is constant (D_a = 0: ctNcc's std is
     // 0, every view's NCC nan, MVS2.py:41-42) passes no view: its outputs are
     // written here (V = [], avg 0) and it is not binned, so the scorers never
-    // see it.  Decided from the scene's moment tables (w nan at V <= 64, D = 0
-    // at V > 64), one gather per candidate, all of a thread's in flight
-    const bool flat_test = mt.sb != nullptr && (mt.w != nullptr || mt.d != nullptr);
-    const bool dtab = mt.d != nullptr;
-    double wk[kBinPer];
-    int dk[kBinPer];
+    // see it.  Decided from the scene's constant-window bits (MomentsDev.flat,
+    // 2 B per pixel and 16 views: an L2 hit), one gather per candidate, all of
+    // a thread's in flight
+    const uint16_t* __restrict__ flat = mt.flat;
+    int fk[kBinPer];
     int qk[kBinPer], rk[kBinPer];
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
         tl[k] = -1;
-        wk[k] = 0.0;
-        dk[k] = 1;
+        fk[k] = 0;
         if (i >= a.n) continue;
         const int R = Rk[k];
         const double c[3] = {ck[k][0], ck[k][1], ck[k][2]};
@@ -513,17 +517,13 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         tl[k] = 0;
         qk[k] = q;
         rk[k] = r;
-        if (flat_test) {
-            const int64_t e = ((int64_t)r * sc.W + q) * mt.VP + R;
-            if (dtab) dk[k] = mt.d[e];
-            else wk[k] = mt.w[e];
-        }
+        if (flat) fk[k] = flat[((int64_t)r * sc.W + q) * (mt.VP >> 4) + (R >> 4)];
     }
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         if (tl[k] < 0) continue;
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        if (flat_test && (dtab ? dk[k] == 0 : wk[k] != wk[k])) {
+        if ((fk[k] >> (Rk[k] & 15)) & 1) {
             tl[k] = -1;
             for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
             if (a.count) a.count[i] = 0;

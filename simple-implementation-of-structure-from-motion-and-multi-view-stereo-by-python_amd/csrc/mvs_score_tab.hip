@@ -29,8 +29,9 @@ namespace {
 // the vertical sums slide down the 16 rows.  The same arithmetic as the
 // in-kernel moments of k_score_mma (the tables are bit-identical to them):
 // D = n Q - S^2 (exact int32), w = v_rsq_f64(D) + one Newton step (a constant
-// window: D = 0, inf, then nan), S_b = S - 128 n.  Stores: lanes = 16 views x
-// 4 pixels, one 128-B row piece of w per pixel.
+// window: D = 0, inf, then nan), S_b = S - 128 n; and a bit per (pixel, view)
+// for D = 0.  Stores: lanes = 16 views x 4 pixels, one 128-B row piece of w
+// per pixel.
 // ---------------------------------------------------------------------------
 constexpr int kMomW = 32, kMomH = 16, kMomV = 16;
 
@@ -98,6 +99,12 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
             const int y = y0 + yl;
             if (y < y_lo || y > y_hi) continue;
             const int64_t o = ((int64_t)y * sc.W + x) * mt.VP + v0 + vi;
+            // the constant windows (D = 0) of the pixel's 16 views as one
+            // 16-bit word: lanes = 16 views x 4 pixels (k_bin's flat test)
+            const uint64_t fb = __ballot(vi < nv && NPX * Q - S * S == 0);
+            if (mt.flat && vi == 0)
+                mt.flat[((int64_t)y * sc.W + x) * (mt.VP / 16) + v0 / 16] =
+                    (uint16_t)(fb >> (16 * ((threadIdx.x >> 4) & 3)));
             if (vi < nv) {
                 const int db = NPX * Q - S * S;
                 mt.sb[o] = (int16_t)(S - 128 * NPX);

@@ -231,6 +231,7 @@ class PointsExchange:
         self.comm = comm_stream if comm_stream is not None else (
             torch.cuda.Stream(self.device) if cuda and (self.world > 1 or self.pack_on_comm) else None)
         self.done = [None, None]
+        self._held = [None, None]
         self.posted = 0
 
     def post(self, offset, count, mask, vlb, stream=None, c=None):
@@ -252,11 +253,14 @@ class PointsExchange:
                 scored = torch.cuda.Event()
                 scored.record(cur)
                 self.comm.wait_event(scored)          # send[b]'s last gather ran on comm itself
-                # the pack reads the slice's outputs on the comm stream: the
-                # caching allocator must not hand them out before it has run
-                for t_ in (count, mask, cc):
-                    if t_ is not None:
-                        t_.record_stream(self.comm)
+                # the pack reads the slice's outputs on the comm stream: they
+                # are held until the next post into buffer b, which orders the
+                # scoring stream after this pack first (a record_stream on the
+                # comm stream instead would leave the caching allocator an event
+                # to record on it after a MaskedStream comm stream is destroyed)
+                if self.read[b] is not None and not self.read[b].query():
+                    cur.wait_event(self.read[b])
+                self._held[b] = (count, mask, cc)
                 self.ctx.pack_accepted(offset, count, mask, vlb, self.send[b], stream=self.comm.cuda_stream, c=cc)
                 rd = torch.cuda.Event()
                 rd.record(self.comm)

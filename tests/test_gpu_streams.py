@@ -41,6 +41,25 @@ def _outputs(rec):
     return r[:, 0].view(np.uint64), np.bitwise_count(r[:, 0].view(np.uint64)).astype(np.int32)
 
 
+EXIT_SCRIPT_SCORE_ONLY = r"""
+import sys, numpy as np, torch, importlib
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {golden!r})
+from make_seeds import load_dino
+pkg = importlib.import_module({pkg!r})
+par = importlib.import_module({pkg!r} + ".parallel")
+imgs, K, R, t = load_dino({data!r})
+ctx = pkg.MvsContext(np.stack(imgs), K, R, t, device=0)
+ms = par.cu_masked_stream("cuda:0", 16)
+c, ref = pkg.synthetic.candidates(1 << 16, K, R, t, seed=3)
+dev = torch.device("cuda:0")
+tc, tr = torch.from_numpy(c).to(dev), torch.from_numpy(ref).to(dev)
+xy = torch.empty((len(ref), 2), dtype=torch.float64, device=dev)
+rec = torch.empty((len(ref), 2), dtype=torch.int64, device=dev)
+ctx.score_device_rec(tc, tr, xy, rec, 0.7, 5, stream=ms.cuda_stream)
+ms.stream.synchronize()
+print("scored", flush=True)
+"""
+
 EXIT_SCRIPT = r"""
 import sys, numpy as np, torch, importlib
 sys.path.insert(0, {repo!r}); sys.path.insert(0, {golden!r})
@@ -66,14 +85,16 @@ print("accepted", ex.accepted()[0], flush=True)
 """
 
 
-def test_masked_stream_exit_without_close(dino):
-    """A masked scoring stream and a masked comm stream used for scoring and
-    the exchange's pack, left open at exit: rc 0, no signal."""
-    code = EXIT_SCRIPT.format(repo=REPO, golden=os.path.join(REPO, "tests", "golden"), pkg=PKG_NAME,
-                              data=os.path.join(REPO, "data", "dinoRing"))
+@pytest.mark.parametrize("script", ["score_only", "score_and_pack"])
+def test_masked_stream_exit_without_close(dino, script):
+    """A masked scoring stream (and a masked comm stream for the exchange's
+    pack) left open at exit: rc 0, no signal."""
+    code = (EXIT_SCRIPT_SCORE_ONLY if script == "score_only" else EXIT_SCRIPT).format(
+        repo=REPO, golden=os.path.join(REPO, "tests", "golden"), pkg=PKG_NAME,
+        data=os.path.join(REPO, "data", "dinoRing"))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
-    assert "accepted" in p.stdout
+    assert ("scored" if script == "score_only" else "accepted") in p.stdout
 
 
 def test_stream_retiring_then_other_streams(pkg, ctx, dino, oracle_scene):
