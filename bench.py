@@ -78,8 +78,9 @@ def floor_bytes(rgb, xy, ref, wid, n):
     valid window whose reference window is not constant (k_bin settles the
     rest), and for them it must read the moment-table rows of their distinct
     pixels (S_b int16 + w binary64 per view at V <= 64, S_b + D int32 at
-    V > 64; VP views per row), the gv regions of their distinct tiles (V views
-    x (8 + 2 wid) rows x 32 B), their bucket entries (8 B) and write their
+    V > 64; VP views per row), the gray bytes of their distinct tiles (V views
+    x 8 x 16 pixels: the regions' halos overlap the neighbours' and are not
+    counted), their bucket entries (8 B) and write their
     records (8 (ceil(V/64) + 1) B).  rgb: (V, H, W, 3) uint8 (host or device); xy, ref:
     device tensors of the sweep.  The windows' constancy is recomputed here
     from integral images of the gray stack (OpenCV's BGR2GRAY weights on the
@@ -116,7 +117,7 @@ def floor_bytes(rgb, xy, ref, wid, n):
     pixels = int(torch.unique(r * W + q).numel())
     ntx = (W + 15) // 16
     tiles = int(torch.unique((r // 8) * ntx + q // 16).numel())
-    parts = {"tables": pixels * vp * (6 if V > 64 else 10), "gv": tiles * V * (8 + 2 * wid) * 32,
+    parts = {"tables": pixels * vp * (6 if V > 64 else 10), "gv": tiles * V * 8 * 16,
              "bucket_entries": 8 * binned, "records": 8 * (words + 1) * binned}
     return sum(parts.values()), parts, {"scored_candidates": binned, "of": n, "distinct_pixels": pixels,
                                         "tiles": tiles}

@@ -111,20 +111,21 @@ int mvs_filter_outliers(int64_t n, int words, int nci, int ncj, const int32_t* c
 /* The multi-GPU sweep's exchange record set (no reference counterpart: the
  * reference is single-process).  The accepted candidates
  * (count >= vlb, MVS2.py:256/369) of a slice of n scored candidates are
- * packed, in index order, into d_out[(cap + 1) * width] int64 with
- * width = 1 + words + (d_c ? 3 : 0): row 0 = [accepted, n, 0...], row 1 + j =
- * [offset + i, mask words of i, and with d_c (the slice's n*3 centres, the
- * candidates' 3D points) the binary64 bits of x, y, z] (40 B at V <= 64;
- * d_c = NULL: 16 B, the receiver regenerating a point from its global index).
+ * packed into d_out[(cap + 1) * width] int64 with width = 1 + words +
+ * (d_c ? 3 : 0): row 0 = [accepted, n, 0...], rows 1.. = [offset + i, mask
+ * words of i, and with d_c (the slice's n*3 centres, the candidates' 3D
+ * points) the binary64 bits of x, y, z] (40 B at V <= 64; d_c = NULL: 16 B,
+ * the receiver regenerating a point from its global index).  Row order: each
+ * chunk of 8,192 candidates in index order, the chunks in the order they
+ * reserve their rows (one atomic each; nothing waits for another chunk), so
+ * the set is exact and the order is not: a receiver that needs index order
+ * sorts by the first column (parallel.PointsExchange.result does).
  * d_count = NULL: d_mask is mvs_score_device_rec's records (words + 1 int64
  * each) and |V| their popcount.
  * Device pointers, stream-ordered, no host synchronisation (the accepted
- * total is in the header; a slice with more than cap accepted keeps its
- * first cap).  The chunks' decoupled look-back never waits unboundedly: a
- * wait that expires (another kernel holding the CUs) takes a slow path that
- * counts the earlier candidates itself, so the rows are always exact;
- * mvs_pack_fallbacks returns how often that happened (synchronises the
- * device).  Feeds the all-gather of parallel.PointsExchange. */
+ * total is in the header; a slice with more than cap accepted keeps cap of
+ * them).  Calls on one context are ordered across streams (their counter is
+ * the context's).  Feeds the all-gather of parallel.PointsExchange. */
 int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_count,
                       const uint64_t* d_mask, const double* d_c, int vlb, int64_t cap, int64_t* d_out,
                       void* stream);
@@ -133,11 +134,6 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
  * 256-thread workgroups on `stream` -- the CU footprint of a collective's
  * kernel, run beside the scoring kernels on one GPU. */
 int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups, void* stream);
-int64_t mvs_pack_fallbacks(mvs_ctx* ctx);
-/* Tests only: mode > 0 sets the pack's look-back spin limit, mode < 0 sends
- * chunk -mode (2,048 candidates each) down the slow path at once, 0 restores
- * the default. */
-int mvs_pack_debug(mvs_ctx* ctx, int64_t mode);
 /* The persistent tiled scorers' grid: `workgroups` > 0 holds them to that
  * many workgroups (at two per CU, the CUs of a CU-masked scoring stream), 0
  * restores the default (every CU, twice).  Multi-GPU steps score on a stream

@@ -39,9 +39,7 @@ SIGNATURES = [
                                             _vp, _vp, _vp]),
     ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
                                          ctypes.c_int64, _vp, _vp]),
-    ("mvs_pack_debug", ctypes.c_int, [_vp, ctypes.c_int64]),
     ("mvs_set_scorer_grid", ctypes.c_int, [_vp, ctypes.c_int]),
-    ("mvs_pack_fallbacks", ctypes.c_int64, [_vp]),
     ("mvs_proxy_copy", ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp]),
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
                                            _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
@@ -370,8 +368,10 @@ class MvsContext:
     def pack_accepted(self, offset, count, mask, vlb, out, stream=None, c=None):
         """mvs_pack_accepted: the accepted candidates (count >= vlb) of a scored
         slice as exchange rows of out (device int64 tensor (cap + 1, width):
-        row 0 = [accepted, n, 0...], then
-        [offset + i, mask words(, x y z bits with c)] in index order); c = the
+        row 0 = [accepted, n, 0...], then rows
+        [offset + i, mask words(, x y z bits with c)]: each 8,192-candidate
+        chunk in index order, the chunks in any order -- sort_rows() orders
+        them); c = the
         slice's (n, 3) float64 centres or None (width 1 + words [+ 3]);
         stream-ordered, no host sync.  count None: mask is score_device_rec's
         records and |V| their popcount."""
@@ -402,19 +402,6 @@ class MvsContext:
         """Hold the persistent scorers to `workgroups` workgroups (0: default,
         two per CU): the grid for a CU-masked scoring stream."""
         check(load().mvs_set_scorer_grid(self._h, int(workgroups)), self._h, "mvs_set_scorer_grid")
-
-    def pack_debug(self, mode=0):
-        """Tests only: the pack's look-back spin limit (mode > 0) or the slow
-        path for chunk -mode (mode < 0); 0 = default."""
-        check(load().mvs_pack_debug(self._h, int(mode)), self._h, "mvs_pack_debug")
-
-    def pack_fallbacks(self):
-        """How many pack chunks took the slow (exact) path since the context
-        was created (synchronises the device)."""
-        r = int(load().mvs_pack_fallbacks(self._h))
-        if r < 0:
-            check(r, self._h, "mvs_pack_fallbacks")
-        return r
 
     def harris_points(self, view):
         """getHarrisPoints(imgs[view]) (HarrisFeatures.py:135-161) on the GPU:

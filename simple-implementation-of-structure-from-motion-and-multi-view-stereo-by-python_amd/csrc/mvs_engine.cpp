@@ -308,12 +308,9 @@ struct mvs_ctx {
     DevBuf<uint64_t> s_mask;
     // tiled scorer scratch
     DevBuf<int32_t> t_tiles, t_cand;
-    // mvs_pack_accepted: the chunks' look-back words (one per MVS_ACC_CHUNK
-    // candidates), their epoch and the give-up counter
-    DevBuf<uint64_t> p_status;
-    DevBuf<int32_t> p_err;
-    uint64_t p_epoch = 0;
-    int64_t pack_debug = 0;   // mvs_pack_debug (tests): spin limit / forced give-up
+    // mvs_pack_accepted: the pack's row counter and chunk ticket (k_acc_pack
+    // leaves both zero)
+    DevBuf<unsigned long long> p_ctl;
     DevBuf<int4> t_items;
     // SfM front-end scratch (Harris maps, descriptors, match rows)
     DevBuf<float> f_resp, f_dil;
@@ -1544,23 +1541,16 @@ int mvs_pack_accepted(mvs_ctx* ctx, int64_t n, int64_t offset, const int32_t* d_
         return set_err(ctx, Fail{MVS_E_ARG, "bad arguments"});
     return guarded(ctx, [&]() {
         hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-        // the pack's own scratch (status words, ticket): ordered against the
+        // the pack's own scratch (counter, ticket): ordered against the
         // previous pack only, so that a pack on a communication stream does
         // not order the next sweep's scoring behind it
         ctx->pack_order.acquire(s);
-        const uint64_t* st_before = ctx->p_status.p;
-        ctx->p_status.ensure(std::max<int64_t>((n + MVS_ACC_CHUNK - 1) / MVS_ACC_CHUNK, 1));
-        if (ctx->p_status.p != st_before) {   // new words: zero, i.e. epoch 0, never used
-            HIPCHK(hipMemsetAsync(ctx->p_status.p, 0, ctx->p_status.n * sizeof(uint64_t), s));
-            ctx->p_epoch = 0;
+        if (!ctx->p_ctl.p) {
+            ctx->p_ctl.ensure(32);
+            HIPCHK(hipMemsetAsync(ctx->p_ctl.p, 0, 32 * sizeof(unsigned long long), s));
         }
-        if (!ctx->p_err.p) {
-            ctx->p_err.ensure(2);   // [0] slow-path chunks, [1] the chunk ticket (k_acc_pack returns it to 0)
-            HIPCHK(hipMemsetAsync(ctx->p_err.p, 0, 2 * sizeof(int32_t), s));
-        }
-        ctx->p_epoch = ctx->p_epoch % ((1ull << 30) - 1) + 1;   // 1 .. 2^30 - 1
-        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, d_c, ctx->words(), vlb, cap, ctx->p_status.p,
-                                     ctx->p_epoch, ctx->p_err.p, ctx->pack_debug, d_out, s) != 0)
+        if (mvs_launch_pack_accepted(n, offset, d_count, d_mask, d_c, ctx->words(), vlb, cap, ctx->p_ctl.p, d_out,
+                                     s) != 0)
             throw Fail{MVS_E_HIP, "pack launch failed"};
         ctx->pack_order.release(s);
         return 0;
@@ -1575,28 +1565,10 @@ int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups
     return 0;
 }
 
-int64_t mvs_pack_fallbacks(mvs_ctx* ctx) {
-    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
-    int32_t h = 0;
-    int rc = guarded(ctx, [&]() {
-        if (!ctx->p_err.p) return 0;
-        HIPCHK(hipDeviceSynchronize());
-        HIPCHK(hipMemcpy(&h, ctx->p_err.p, sizeof h, hipMemcpyDeviceToHost));
-        return 0;
-    });
-    return rc ? rc : h;
-}
-
 int mvs_set_scorer_grid(mvs_ctx* ctx, int workgroups) {
     if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
     if (workgroups < 0) return set_err(ctx, Fail{MVS_E_ARG, "workgroups must be >= 0"});
     ctx->scorer_wgs = workgroups;
-    return 0;
-}
-
-int mvs_pack_debug(mvs_ctx* ctx, int64_t mode) {
-    if (!ctx) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
-    ctx->pack_debug = mode;
     return 0;
 }
 

@@ -192,7 +192,7 @@ struct ExpandArgs {
 #ifndef MVS_ACC_PER
 #define MVS_ACC_PER 8         // candidates per thread of the exchange's pack (A/B switch)
 #endif
-#define MVS_ACC_CHUNK (256 * MVS_ACC_PER)   // candidates per chunk of the exchange's pack (k_acc_pack)
+#define MVS_ACC_CHUNK (1024 * MVS_ACC_PER)   // candidates per chunk of the exchange's pack (k_acc_pack)
 
 extern "C" {
 // RGB -> stack and gv (one pass, coalesced on both sides); the caller zeroes
@@ -230,16 +230,14 @@ int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hipStream_t s)
 // of children whose masks another rank scored (geometry already in place)
 int mvs_launch_expand_ingest(RecordsDev rec, const ExpandArgs* a, int words, hipStream_t s);
 // The accepted candidates of a sweep slice as exchange rows [global index,
-// mask words, (c != null) x y z bits] after a header row [accepted, n, 0...],
-// in index order, at most cap rows (parallel.PointsExchange), one launch;
+// mask words, (c != null) x y z bits] after a header row [accepted, n, 0...]
+// (each chunk of MVS_ACC_CHUNK candidates in index order, chunks in the order
+// they reserve rows), at most cap rows (parallel.PointsExchange), one launch;
 // count == null: mask holds records of words + 1 int64 and |V| is their
-// popcount; status holds max(ceil(n / MVS_ACC_CHUNK), 1) words of the chunks'
-// look-back, epoch in [1, 2^30) differs from the previous call's on the same
-// status buffer, *err counts look-back waits that expired and took the slow,
-// exact path; debug: see k_acc_pack (0 in production)
+// popcount; ctl: the pack's counter ([0]) and chunk ticket ([16]), zero
+// before the call and left zero after it
 int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask, const double* c,
-                             int words, int vlb, int64_t cap, uint64_t* status, uint64_t epoch, int32_t* err,
-                             int64_t debug, int64_t* out, hipStream_t s);
+                             int words, int vlb, int64_t cap, unsigned long long* ctl, int64_t* out, hipStream_t s);
 // measurement only: a copy of bytes (multiple of 16) by `workgroups` workgroups
 int mvs_launch_proxy_copy(void* dst, const void* src, int64_t bytes, int workgroups, hipStream_t s);
 int mvs_launch_ncc_windows(int64_t n, int npx, const uint8_t* a, const uint8_t* b, double thr,

@@ -2111,257 +2111,154 @@ __global__ void k_expand_ingest(RecordsDev rec, const ExpandArgs a, int words) {
 
 // ---------------------------------------------------------------------------
 // The multi-GPU sweep's exchange record set (parallel.PointsExchange): the
-// accepted candidates of a rank's slice (|V| >= vlb, MVS2.py:256/369) packed
-// in index order into rows [global index, mask words..., (c) x, y, z as
-// binary64 bits] of a fixed-capacity buffer whose row 0 is the header
-// [accepted, n, 0...].  No host synchronisation: the accepted total travels in
-// the header, and a slice with more than cap accepted candidates keeps its
-// first cap rows (the receiver sees accepted > cap).  Each chunk's rows go to
-// (sum of the earlier chunks' counts) + their rank.
+// accepted candidates of a rank's slice (|V| >= vlb, MVS2.py:256/369) as rows
+// [global index, mask words..., (c) x, y, z as binary64 bits] of a
+// fixed-capacity buffer whose row 0 is the header [accepted, n, 0...].  No
+// host synchronisation: the accepted total travels in the header, and a slice
+// with more than cap accepted candidates keeps cap of them (the receiver sees
+// accepted > cap).
+// One workgroup per chunk of kAccChunk = 8,192 candidates (thread t holds
+// candidates chunk + t + 1024 j, j < kAccPer: coalesced loads).  A chunk's
+// rows are its accepted candidates in index order; the chunks reserve their
+// row ranges by one returning atomic each on the pack's counter, in whatever
+// order they get there -- no chunk waits for another (round 5's decoupled
+// look-back kept the rows in index order across chunks and cost ~18 us per
+// 2^20 sweep); the receiver orders rows by their index column if it needs
+// to (PointsExchange.result).  The workgroup that takes the last ticket
+// writes the header and returns the counter and the ticket to zero for the
+// next call.
 // ---------------------------------------------------------------------------
-// Chunks of kAccPer x kAccThreads = 2,048 candidates, thread t of a chunk
-// holding candidates chunk + t + kAccThreads j (j < kAccPer): the reads stay
-// coalesced, a 2^20 slice has 512 chunks (two workgroups on every CU), and
-// the look-back reads 512-chunk windows (one window for such a slice).  Each candidate's first
-// mask word is loaded with its count (records: the count IS its popcount), the
-// accepted candidates' points as soon as the counts are in; they stay in
-// flight across the chunk's scan and look-back (LDS-only barriers), so that
-// the rows go out as soon as the prefix is in.
-constexpr int kAccThreads = 256, kAccPer = MVS_ACC_PER, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
+constexpr int kAccThreads = 1024, kAccPer = MVS_ACC_PER, kAccChunk = kAccThreads * kAccPer, kAccWaves = kAccThreads / 64;
 constexpr int kAccE = kAccPer * kAccWaves;          // (j, wave) counts of a chunk
 constexpr int kAccEpl = (kAccE + 63) / 64;          // of them per lane of wave 0's scan
-constexpr int kAccLB = 8;                            // status words per lane of the look-back window
 // 16-B accesses at 8-B alignment (global_load/store_dwordx4 allow it)
 typedef double acc_d2v __attribute__((ext_vector_type(2)));
 typedef acc_d2v acc_d2 __attribute__((aligned(8)));
 typedef long long acc_l2v __attribute__((ext_vector_type(2)));
 typedef acc_l2v acc_l2 __attribute__((aligned(8)));
-static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the status words by MVS_ACC_CHUNK");
+static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the pack's grid by MVS_ACC_CHUNK");
 static_assert(kAccE <= 128, "wave 0 scans at most two (j, wave) counts per lane");
 
-// One launch: each chunk's rows start after every earlier chunk's accepted
-// count, found by a decoupled look-back over per-chunk status words
-// (epoch << 34 | flag << 32 | value; flag 1 = the chunk's own count, 2 = the
-// inclusive count through it; a word of another epoch is not yet published).
-// One workgroup per chunk, dispatched in index order, so a chunk waits only
-// for earlier chunks' workgroups, which have started (however many chunks
-// there are); but a kernel sharing the CUs (RCCL's, the next sweep's scorer)
-// can delay them, so every wait is bounded in time (kAccWaitTicks of the
-// 100 MHz real-time clock, the wave sleeping between polls):
-// on expiry the chunk takes the slow path that depends on no other workgroup
-// -- the whole workgroup counts the accepted candidates before it from the
-// inputs -- and publishes that exact prefix (so no result is ever wrong);
-// *err counts these fall-backs (mvs_pack_fallbacks).  The words are relaxed
-// agent-scope atomics: a word carries all a reader needs, and a release or
-// acquire would write back or invalidate this XCD's L2 at every step.
-// debug (tests only): > 0 = a limit in polls; < 0 = chunk -debug falls back at once.
-constexpr uint64_t kAccWaitTicks = 20000;            // 200 us
-
-DEV int acc_count(const int32_t* __restrict__ count, const uint64_t* __restrict__ mask, int64_t ms, int words,
-                  int64_t i) {
-    if (count) return count[i];
-    int c = 0;
-    for (int q = 0; q < words; ++q) c += __popcll(mask[i * ms + q]);
-    return c;
-}
-
+// ctl: [0] the row counter, [16] the chunk ticket (128 B apart), both zero
+// between calls
 __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
                                                           const uint64_t* __restrict__ mask, const double* __restrict__ cpt,
-                                                          int words, int vlb, int64_t cap, uint64_t* __restrict__ status,
-                                                          uint64_t epoch, int32_t* __restrict__ err, int64_t debug,
+                                                          int words, int vlb, int64_t cap,
+                                                          unsigned long long* __restrict__ ctl,
                                                           int64_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) int32_t s_cnt[kAccPer * kAccWaves];   // accepted per (j, wave), then their exclusive prefix
+    __shared__ __attribute__((aligned(16))) int32_t s_cnt[kAccE];   // accepted per (j, wave), then their exclusive prefix
     __shared__ int64_t s_base;
-    __shared__ int s_slow;
-    __shared__ int64_t s_total;
-    __shared__ int64_t s_part[kAccWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int width = 1 + words + (cpt ? 3 : 0);
     // count == null: the scorer's records [mask words, avg], |V| = popcount
     const int64_t ms = count ? words : words + 1;
-    const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
-    const int64_t nch = nchunk > 0 ? nchunk : 1;      // an empty slice still has chunk 0, which writes the header
-    const uint64_t E = epoch << 34;
-    {
-        const int64_t b = blockIdx.x;
-        // every load of the chunk in flight at once: the first mask words and
-        // the counts (records: popcounts of the words)
-        uint64_t m[kAccPer], w0[kAccPer];
-        int c[kAccPer];
+    const int64_t nch = max((n + kAccChunk - 1) / kAccChunk, (int64_t)1);   // an empty slice still writes the header
+    const int64_t b = blockIdx.x;
+    // every load of the chunk in flight at once: the first mask words and the
+    // counts (records: popcounts of the words)
+    uint64_t m[kAccPer], w0[kAccPer];
+    int c[kAccPer];
 #pragma unroll
-        for (int j = 0; j < kAccPer; ++j) {
+    for (int j = 0; j < kAccPer; ++j) {
+        const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+        w0[j] = i < n ? mask[i * ms] : 0ull;
+        c[j] = i < n && count ? count[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kAccPer; ++j) {
+        const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+        if (i < n && !count) {
+            c[j] = __popcll(w0[j]);
+            for (int q = 1; q < words; ++q) c[j] += __popcll(mask[i * ms + q]);
+        }
+    }
+    // the accepted candidates' points, in flight across the scan and the
+    // reservation (LDS-only barriers)
+    double px[kAccPer], py[kAccPer], pz[kAccPer];
+#pragma unroll
+    for (int j = 0; j < kAccPer; ++j) {
+        const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
+        const bool acc = i < n && c[j] >= vlb;
+        m[j] = __ballot(acc);
+        px[j] = py[j] = pz[j] = 0.0;
+        if (cpt && acc) {
+            // x, y as one 16-B load (8-B aligned), z beside it
+            const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
+            px[j] = xy.x;
+            py[j] = xy.y;
+            pz[j] = cpt[3 * i + 2];
+        }
+        if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
+    }
+    lds_barrier();
+    if (wave == 0) {
+        // exclusive scan of the (j, wave) counts in index order, kAccEpl
+        // consecutive ones per lane
+        int x[kAccEpl], tot = 0;
+#pragma unroll
+        for (int q = 0; q < kAccEpl; ++q) {
+            const int e = lane * kAccEpl + q;
+            x[q] = e < kAccE ? s_cnt[e] : 0;
+            tot += x[q];
+        }
+        int incl = tot;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        int ex = incl - tot;
+#pragma unroll
+        for (int q = 0; q < kAccEpl; ++q) {
+            const int e = lane * kAccEpl + q;
+            if (e < kAccE) s_cnt[e] = ex;
+            ex += x[q];
+        }
+        const unsigned long long T = (unsigned)__shfl(incl, 63, 64);   // this chunk's accepted
+        if (lane == 0) {
+            // this chunk's rows, then its ticket (after the reservation has
+            // returned: the last ticket sees every chunk's rows counted)
+            const unsigned long long base = T ? atomicAdd(&ctl[0], T) : 0ull;
+            s_base = (int64_t)base;
+            // the ticket's address depends on the reservation's result (always
+            // 0 + 16; opaque to the compiler), so it issues after the return
+            const int dep = opaque((int)(base >> 63));
+            const unsigned long long tk = atomicAdd(&ctl[16 + dep], 1ull);
+            if ((int64_t)tk == nch - 1) {
+                const int64_t total = (int64_t)__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                out[0] = total;
+                out[1] = n;
+                for (int q = 2; q < width; ++q) out[q] = 0;
+                __hip_atomic_store(&ctl[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl[16], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    lds_barrier();
+    const int64_t base = s_base;
+#pragma unroll
+    for (int j = 0; j < kAccPer; ++j) {
+        if ((m[j] >> lane) & 1ull) {
             const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            w0[j] = i < n ? mask[i * ms] : 0ull;
-            c[j] = i < n && count ? count[i] : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < kAccPer; ++j) {
-            const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            if (i < n && !count) {
-                c[j] = __popcll(w0[j]);
-                for (int q = 1; q < words; ++q) c[j] += __popcll(mask[i * ms + q]);
-            }
-        }
-        double px[kAccPer], py[kAccPer], pz[kAccPer];
-#pragma unroll
-        for (int j = 0; j < kAccPer; ++j) {
-            const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-            const bool acc = i < n && c[j] >= vlb;
-            m[j] = __ballot(acc);
-            px[j] = py[j] = pz[j] = 0.0;
-            if (cpt && acc) {
-                // x, y as one 16-B load (8-B aligned), z beside it
-                const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
-                px[j] = xy.x;
-                py[j] = xy.y;
-                pz[j] = cpt[3 * i + 2];
-            }
-            if (lane == 0) s_cnt[j * kAccWaves + wave] = __popcll(m[j]);
-        }
-        lds_barrier();   // the points stay in flight
-        if (wave == 0) {
-            // exclusive scan of the (j, wave) counts in index order, kAccEpl
-            // consecutive ones per lane
-            int x[kAccEpl], tot = 0;
-#pragma unroll
-            for (int q = 0; q < kAccEpl; ++q) {
-                const int e = lane * kAccEpl + q;
-                x[q] = e < kAccE ? s_cnt[e] : 0;
-                tot += x[q];
-            }
-            int incl = tot;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int y = __shfl_up(incl, off, 64);
-                if (lane >= off) incl += y;
-            }
-            int ex = incl - tot;
-#pragma unroll
-            for (int q = 0; q < kAccEpl; ++q) {
-                const int e = lane * kAccEpl + q;
-                if (e < kAccE) s_cnt[e] = ex;
-                ex += x[q];
-            }
-            const uint64_t T = (uint32_t)__shfl(incl, 63, 64);   // this chunk's accepted
-            // publish, then look back over the kAccLB x 64 chunks before b at
-            // a time (a 2^20 slice's 512 chunks in one window: one round of
-            // status loads once the predecessors have published)
-            if (lane == 0)
-                __hip_atomic_store(&status[b], E | ((b == 0 ? 2ull : 1ull) << 32) | T, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t excl = 0;
-            int64_t top = b - 1;          // the window's highest chunk
-            uint32_t polls = 0;
-            uint64_t t_start = 0;
-            bool slow = debug < 0 && b == -debug;
-            constexpr int WIN = 64 * kAccLB;
-            while (top >= 0 && !slow) {
-                // lane l, word j: chunk top - (64 j + l), at distance 64 j + l
-                uint64_t v[kAccLB];
-#pragma unroll
-                for (int j = 0; j < kAccLB; ++j) {
-                    const int64_t k = top - lane - 64 * j;
-                    v[j] = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : (E | (2ull << 32));
-                }
-                // the nearest inclusive word, and whether every chunk up to it has published
-                int d_incl = WIN, d_unpub = WIN;
-#pragma unroll
-                for (int j = 0; j < kAccLB; ++j) {
-                    const bool pub = (v[j] & ~((1ull << 34) - 1)) == E;
-                    const uint32_t flag = pub ? (uint32_t)(v[j] >> 32) & 3u : 0u;
-                    const uint64_t im = __ballot(flag == 2), um = __ballot(!pub);
-                    if (d_incl == WIN && im) d_incl = 64 * j + __builtin_ctzll(im);
-                    if (d_unpub == WIN && um) d_unpub = 64 * j + __builtin_ctzll(um);
-                }
-                if (d_unpub < d_incl) {
-                    // a chunk in the window has not published yet
-                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                    if (polls++ == 0) t_start = now;
-                    if (debug > 0 ? polls > (uint32_t)debug : now - t_start > kAccWaitTicks) slow = true;
-                    __builtin_amdgcn_s_sleep(2);
-                    continue;
-                }
-                // the published words at distances 0..d_incl
-                uint64_t val = 0;
-#pragma unroll
-                for (int j = 0; j < kAccLB; ++j)
-                    if (64 * j + lane <= d_incl && top - lane - 64 * j >= 0) val += v[j] & 0xffffffffull;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
-                excl += val;
-                if (d_incl < WIN) break;        // reached an inclusive prefix
-                top -= WIN;
-            }
-            if (lane == 0) {
-                if (!slow) {
-                    // the inclusive prefix, and the header from the last chunk
-                    if (b > 0)
-                        __hip_atomic_store(&status[b], E | (2ull << 32) | (excl + T), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    if (b == nch - 1) {
-                        out[0] = (int64_t)(excl + T);   // accepted in the whole slice
-                        out[1] = n;
-                        for (int q = 2; q < width; ++q) out[q] = 0;
-                    }
-                }
-                s_slow = slow ? 1 : 0;
-                s_base = (int64_t)excl;
-                s_total = (int64_t)T;
-            }
-        }
-        lds_barrier();
-        if (s_slow) {
-            // the slow path: the accepted candidates of [0, b chunk) counted
-            // from the inputs by the whole workgroup (no other workgroup involved)
-            int64_t part = 0;
-            for (int64_t i = threadIdx.x; i < b * kAccChunk; i += kAccThreads)
-                part += acc_count(count, mask, ms, words, i) >= vlb ? 1 : 0;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
-            if (lane == 0) s_part[wave] = part;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                int64_t excl = 0;
-                for (int w = 0; w < kAccWaves; ++w) excl += s_part[w];
-                const int64_t T = s_total;
-                __hip_atomic_store(&status[b], E | (2ull << 32) | (uint64_t)(excl + T), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                if (b == nch - 1) {
-                    out[0] = excl + T;
-                    out[1] = n;
-                    for (int q = 2; q < width; ++q) out[q] = 0;
-                }
-                s_base = excl;
-                __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
-        }
-        const int64_t base = s_base;
-#pragma unroll
-        for (int j = 0; j < kAccPer; ++j) {
-            if ((m[j] >> lane) & 1ull) {
-                const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
-                const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
-                                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
-                if (pos < cap && words == 1 && cpt) {
-                    // the 40-B row as 16 + 16 + 8 B (8-B aligned stores)
-                    int64_t* o = out + (1 + pos) * width;
-                    *(acc_l2*)o = acc_l2{offset + i, (int64_t)w0[j]};
-                    *(acc_l2*)(o + 2) = acc_l2{__double_as_longlong(px[j]), __double_as_longlong(py[j])};
-                    o[4] = __double_as_longlong(pz[j]);
-                } else if (pos < cap) {
-                    int64_t* o = out + (1 + pos) * width;
-                    o[0] = offset + i;
-                    o[1] = (int64_t)w0[j];
-                    for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
-                    if (cpt) {
-                        // the accepted 3D point itself (binary64 bits)
-                        o[1 + words] = __double_as_longlong(px[j]);
-                        o[2 + words] = __double_as_longlong(py[j]);
-                        o[3 + words] = __double_as_longlong(pz[j]);
-                    }
+            const int64_t pos = base + s_cnt[j * kAccWaves + wave] +
+                                __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
+            if (pos < cap && words == 1 && cpt) {
+                // the 40-B row as 16 + 16 + 8 B (8-B aligned stores)
+                int64_t* o = out + (1 + pos) * width;
+                *(acc_l2*)o = acc_l2{offset + i, (int64_t)w0[j]};
+                *(acc_l2*)(o + 2) = acc_l2{__double_as_longlong(px[j]), __double_as_longlong(py[j])};
+                o[4] = __double_as_longlong(pz[j]);
+            } else if (pos < cap) {
+                int64_t* o = out + (1 + pos) * width;
+                o[0] = offset + i;
+                o[1] = (int64_t)w0[j];
+                for (int q = 1; q < words; ++q) o[1 + q] = (int64_t)mask[i * ms + q];
+                if (cpt) {
+                    // the accepted 3D point itself (binary64 bits)
+                    o[1 + words] = __double_as_longlong(px[j]);
+                    o[2 + words] = __double_as_longlong(py[j]);
+                    o[3 + words] = __double_as_longlong(pz[j]);
                 }
             }
         }
@@ -2721,14 +2618,14 @@ extern "C" int mvs_launch_expand_accept(RecordsDev rec, const ExpandArgs* a, hip
 }
 
 extern "C" int mvs_launch_pack_accepted(int64_t n, int64_t offset, const int32_t* count, const uint64_t* mask,
-                                        const double* c, int words, int vlb, int64_t cap, uint64_t* status,
-                                        uint64_t epoch, int32_t* err, int64_t debug, int64_t* out, hipStream_t s) {
+                                        const double* c, int words, int vlb, int64_t cap, unsigned long long* ctl,
+                                        int64_t* out, hipStream_t s) {
     const int64_t nchunk = (n + kAccChunk - 1) / kAccChunk;
     if (nchunk >= ((int64_t)1 << 31)) return -3;
     const int grid = (int)std::max<int64_t>(1, nchunk);   // one workgroup per chunk
     // n == 0 still writes the header (chunk 0 of an empty slice)
     hipLaunchKernelGGL(k_acc_pack, dim3(grid), dim3(kAccThreads), 0, s, n, offset, count, mask, c, words, vlb, cap,
-                       status, epoch, err, debug, out);
+                       ctl, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

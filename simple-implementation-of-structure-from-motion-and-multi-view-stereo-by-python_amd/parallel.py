@@ -168,6 +168,14 @@ def points_width(words, points=True):
     return 1 + words + (3 if points else 0)
 
 
+def sort_rows(rows):
+    """Exchange rows (k, width) int64 ordered by their global index (column
+    0): mvs_pack_accepted leaves its chunks in reservation order."""
+    if rows.shape[0] == 0:
+        return rows
+    return rows[torch.argsort(rows[:, 0], stable=True)]
+
+
 def pack_accepted_reference(offset, count, mask, vlb, out, c=None):
     """mvs_pack_accepted's layout from torch ops, for CPU tensors only (the
     gloo process groups of the CPU tests): header [accepted, n, 0...], then
@@ -195,7 +203,8 @@ def pack_accepted_reference(offset, count, mask, vlb, out, c=None):
 
 class PointsExchange:
     """Per-sweep all-gather of the accepted points as
-    [global index, mask words, x, y, z] rows (points=False: without the
+    [global index, mask words, x, y, z] rows, in chunk order (result() sorts
+    them by index) (points=False: without the
     point, which then follows from the index), pipelined: post() packs this
     rank's accepted rows on the scoring stream (no host sync) and starts the
     all-gather on a communication stream that waits only for that pack, so
@@ -316,7 +325,8 @@ class PointsExchange:
         (host sync; a consumer of the exchange, not the timed loop):
         (global index, mask (k, words) int64 view[, points (k, 3) float64])."""
         blk = self.check(b)
-        rows = torch.cat([blk[r, 1:1 + int(blk[r, 0, 0])] for r in range(blk.shape[0])])
+        # every rank's rows in index order (the pack orders them per chunk only)
+        rows = torch.cat([sort_rows(blk[r, 1:1 + int(blk[r, 0, 0])]) for r in range(blk.shape[0])])
         if self.points:
             pts = rows[:, 1 + self.words:4 + self.words].contiguous().view(torch.float64)
             return rows[:, 0], rows[:, 1:1 + self.words], pts

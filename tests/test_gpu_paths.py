@@ -273,12 +273,14 @@ def test_timed_kernel_name(ctx, dino):
 
 def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     """mvs_pack_accepted (the multi-GPU exchange's device pack, no host sync)
-    against parallel.pack_accepted_reference on the bench's 2^20 sweep:
-    identical header and rows -- with the accepted 3D points (40-B rows, the
-    bench's exchange) and without (16-B rows) -- including a capacity below the
-    accepted count (the first cap rows, the true count in the header) and an
-    empty slice.  The pack's device time per call is printed (launch gaps
-    included; bound 30 us per 2^20 sweep)."""
+    against parallel.pack_accepted_reference on the bench's 2^20 sweep: the
+    same header and the same rows once ordered by index (the pack keeps each
+    8,192-candidate chunk in index order, the chunks in reservation order) --
+    with the accepted 3D points (40-B rows, the bench's exchange) and without
+    (16-B rows) -- including a capacity below the accepted count (cap distinct
+    accepted rows, the true count in the header) and an empty slice.  The
+    pack's device time per call is printed and bounded (15 us per 2^20 sweep,
+    launch gaps included)."""
     import importlib
     import torch
     par = importlib.import_module(pkg.__name__ + ".parallel")
@@ -296,20 +298,26 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
     assert acc > 1000
     for pts in (False, True):
         w = par.points_width(1, pts)
+        exp = torch.full((acc + 1, w), -9, dtype=torch.int64)
         for cap, off in ((acc + 300, 5 << 20), (acc // 3, 0)):
             out = torch.full((cap + 1, w), -9, dtype=torch.int64, device=dev)
             torch.cuda.synchronize()
             ctx.pack_accepted(off, count, mask, 3, out, c=tc if pts else None)   # the library's stream
             torch.cuda.synchronize()
-            exp = torch.full((cap + 1, w), -9, dtype=torch.int64)
             par.pack_accepted_reference(off, count.cpu(), mask.cpu(), 3, exp, torch.from_numpy(c) if pts else None)
             got = out.cpu()
             k = min(acc, cap)
             assert got[0].tolist() == [acc, n] + [0] * (w - 2)
-            assert torch.equal(got[1:1 + k], exp[1:1 + k])
+            rows = par.sort_rows(got[1:1 + k])
+            if cap >= acc:
+                assert torch.equal(rows, exp[1:1 + acc])
+                assert (got[1 + acc:] == -9).all()
+            else:   # cap rows, each one of the accepted rows, none twice
+                pos = torch.searchsorted(exp[1:, 0].contiguous(), rows[:, 0].contiguous())
+                assert torch.equal(rows, exp[1:][pos]) and int(torch.unique(rows[:, 0]).numel()) == k
             if pts:   # the rows carry the candidates' own centres, bit for bit
-                idx = got[1:1 + k, 0].numpy() - off
-                assert np.array_equal(got[1:1 + k, 2:5].contiguous().view(torch.float64).numpy(), c[idx])
+                idx = rows[:, 0].numpy() - off
+                assert np.array_equal(rows[:, 2:5].contiguous().view(torch.float64).numpy(), c[idx])
     empty = torch.full((4, 2), -9, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     ctx.pack_accepted(0, count[:0], mask[:0], 3, empty)
@@ -338,19 +346,18 @@ def test_pack_accepted_vs_reference_and_time(pkg, ctx, dino):
         print(f"pack_accepted ({'40' if pts else '16'}-B rows): {us:.1f} us per 2^20 sweep ({acc} accepted rows)")
         assert int(out[0, 0]) == acc
         # events around back-to-back launches include the inter-kernel gaps;
-        # the kernel's own time is in the rocprof summaries (profiles/r04/)
-        assert us <= 30.0
+        # the kernel's own time is in the rocprof summaries (profiles/r06/)
+        assert us <= 15.0
 
 
-@pytest.mark.parametrize("n", [1, 2047, 2049, 200_001, 5_000_001])
-def test_pack_accepted_lookback_sizes(pkg, ctx, n):
-    """The pack's one-launch look-back over 2,048-candidate chunks (one
-    workgroup each): a single partial chunk, a chunk boundary, several
-    look-back windows (98 chunks at 200k), and more chunks (2,442 at 5M) than
-    workgroups resident at once, so that chunks wait on predecessors
-    dispatched in earlier rounds; synthetic counts/masks against the torch
-    reference, twice in a row (the status words' epoch changes between
-    calls)."""
+@pytest.mark.parametrize("n", [1, 8191, 8193, 200_001, 5_000_001])
+def test_pack_accepted_sizes(pkg, ctx, n):
+    """The pack over 8,192-candidate chunks (one workgroup each, one row
+    reservation each): a single partial chunk, a chunk boundary, 25 chunks,
+    and more chunks (611 at 5M) than workgroups resident at once; synthetic
+    counts/masks against the torch reference, three calls in a row on two
+    streams with an empty slice between them (the counter and the ticket
+    must come back to zero after every call)."""
     import importlib
     import torch
     par = importlib.import_module(pkg.__name__ + ".parallel")
@@ -361,50 +368,22 @@ def test_pack_accepted_lookback_sizes(pkg, ctx, n):
     exp = torch.full((acc + 2, 2), -9, dtype=torch.int64)
     par.pack_accepted_reference(7, count, mask, 3, exp)
     dc, dm = count.cuda(), mask.cuda()
-    for _ in range(2):
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for k in range(3):
         out = torch.full((acc + 2, 2), -9, dtype=torch.int64, device="cuda")
-        # the library's own stream (torch's default stream is handle 0, which
-        # the C-ABI reads as "no stream"): synchronise the device around it
         torch.cuda.synchronize()
-        ctx.pack_accepted(7, dc, dm, 3, out)
+        s = streams[k & 1]
+        ctx.pack_accepted(7, dc, dm, 3, out, stream=s.cuda_stream)
+        if k == 1:
+            e = torch.full((2, 2), -9, dtype=torch.int64, device="cuda")
+            ctx.pack_accepted(0, dc[:0], dm[:0], 3, e, stream=streams[0].cuda_stream)
         torch.cuda.synchronize()
         got = out.cpu()
         assert got[0].tolist() == [acc, n]
-        assert torch.equal(got[1:1 + acc], exp[1:1 + acc])
-
-
-def test_pack_lookback_expiry_stays_exact(pkg, ctx):
-    """A look-back wait that expires (another kernel can hold the
-    CUs the earlier chunks need) must not corrupt the exchange: the chunk takes
-    the slow path that counts its prefix itself.  Forced for chunk 3, and with
-    a spin limit of one iteration over 489 chunks: the header and every row
-    stay exact, and mvs_pack_fallbacks counts the slow chunks."""
-    import importlib
-    import torch
-    par = importlib.import_module(pkg.__name__ + ".parallel")
-    n = 1_000_001
-    g = torch.Generator().manual_seed(3)
-    count = torch.randint(0, 8, (n,), generator=g, dtype=torch.int32)
-    mask = torch.randint(-2**62, 2**62, (n, 1), generator=g, dtype=torch.int64)
-    acc = int((count >= 3).sum())
-    exp = torch.full((acc + 2, 2), -9, dtype=torch.int64)
-    par.pack_accepted_reference(0, count, mask, 3, exp)
-    dc, dm = count.cuda(), mask.cuda()
-    f0 = ctx.pack_fallbacks()
-    try:
-        for mode in (-3, 1, 0):
-            ctx.pack_debug(mode)
-            out = torch.full((acc + 2, 2), -9, dtype=torch.int64, device="cuda")
-            torch.cuda.synchronize()
-            ctx.pack_accepted(0, dc, dm, 3, out)
-            torch.cuda.synchronize()
-            got = out.cpu()
-            assert got[0].tolist() == [acc, n], mode
-            assert torch.equal(got[1:1 + acc], exp[1:1 + acc]), mode
-            if mode == -3:
-                assert ctx.pack_fallbacks() == f0 + 1
-    finally:
-        ctx.pack_debug(0)
+        assert torch.equal(par.sort_rows(got[1:1 + acc]), exp[1:1 + acc])
+        assert got[1 + acc].tolist() == [-9, -9]
+        if k == 1:
+            assert e[0].cpu().tolist() == [0, 0]
 
 
 def test_score_records_vs_arrays_and_pack(pkg, ctx, dino, orc):
@@ -449,10 +428,12 @@ def test_score_records_vs_arrays_and_pack(pkg, ctx, dino, orc):
         ctx.pack_accepted(3, count, mask, 3, o1, c=tc)
         ctx.pack_accepted(3, None, rec, 3, o2, c=tc)
         torch.cuda.synchronize()
-        assert int(o1[0, 0]) == acc and torch.equal(o1, o2)
+        r1, r2 = o1.cpu(), o2.cpu()
+        assert int(r1[0, 0]) == acc and torch.equal(r1[0], r2[0])
+        assert torch.equal(par.sort_rows(r1[1:1 + acc]), par.sort_rows(r2[1:1 + acc]))
         exp = torch.full((acc + 5, w), -9, dtype=torch.int64)
         par.pack_accepted_reference(3, None, rec.cpu(), 3, exp, torch.from_numpy(c))
-        assert torch.equal(o2.cpu()[:1 + acc], exp[:1 + acc])
+        assert torch.equal(r2[0], exp[0]) and torch.equal(par.sort_rows(r2[1:1 + acc]), exp[1:1 + acc])
 
 
 def test_skewed_batch_overflow_cost(pkg, ctx, dino, orc):
