@@ -34,18 +34,20 @@ DEV void project(const CamDev& cm, const double* c, double& px, double& py) {
     py = y * cm.fy + cm.cy;
 }
 
-// The same projection from 16 values [R' (9), t (3), fx, fy, cx, cy] (k_bin
-// keeps them in LDS); identical operations in the same order.
-DEV void project_vals(const double* cv, const double* c, double& px, double& py) {
+// The same projection from 16 values [R' (9), t (3), fx, fy, cx, cy], value
+// k = cv(k) (k_bin keeps them in LDS, field-major); identical operations in
+// the same order.
+template <class CV>
+DEV void project_vals(CV&& cv, const double* c, double& px, double& py) {
     const double X = c[0], Y = c[1], Z = c[2];
-    double x = cv[0] * X + cv[1] * Y + cv[2] * Z + cv[9];
-    double y = cv[3] * X + cv[4] * Y + cv[5] * Z + cv[10];
-    double z = cv[6] * X + cv[7] * Y + cv[8] * Z + cv[11];
+    double x = cv(0) * X + cv(1) * Y + cv(2) * Z + cv(9);
+    double y = cv(3) * X + cv(4) * Y + cv(5) * Z + cv(10);
+    double z = cv(6) * X + cv(7) * Y + cv(8) * Z + cv(11);
     z = z != 0.0 ? 1.0 / z : 1.0;
     x *= z;
     y *= z;
-    px = x * cv[12] + cv[14];
-    py = y * cv[13] + cv[15];
+    px = x * cv(12) + cv(14);
+    py = y * cv(13) + cv(15);
 }
 
 // getDescFeatures bounds (HarrisFeatures.py:128), row = y, col = x.

@@ -125,7 +125,10 @@ struct TiledArgs {
 #ifndef MVS_BIN_PER
 #define MVS_BIN_PER 4
 #endif
-#define MVS_BIN_CHUNK (1024 * MVS_BIN_PER)
+#ifndef MVS_BIN_BLOCK
+#define MVS_BIN_BLOCK 1024   // threads per k_bin workgroup (tuning constant)
+#endif
+#define MVS_BIN_CHUNK (MVS_BIN_BLOCK * MVS_BIN_PER)
 // Per-scene window moments of the tiled scorers, one table pair per window
 // half-width, built once from the gray stack (k_moments): for pixel (y, x)
 // with a valid window and view v, element (y * W + x) * VP + v holds

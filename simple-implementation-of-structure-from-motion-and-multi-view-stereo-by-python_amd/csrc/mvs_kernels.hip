@@ -405,7 +405,7 @@ __device__ unsigned long long g_stamps[4096 * 16];
 #define STAMP_ADD_LANE0(slot, val)
 #endif
 
-constexpr int kBinBlock = 1024, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
+constexpr int kBinBlock = MVS_BIN_BLOCK, kBinPer = MVS_BIN_PER, kBinLdsTiles = 16384;
 static_assert(kBinBlock * kBinPer == MVS_BIN_CHUNK, "MVS_BIN_CHUNK candidates per k_bin workgroup");
 static_assert(kBinBlock * kBinPer <= 4096, "k_bin_count packs a rank inside the workgroup into 12 bits");
 #ifndef MVS_IMPLICIT_MEAN
@@ -459,13 +459,16 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     extern __shared__ int32_t hist[];      // [ntiles] local counts, then global bases
     // the cameras' projection constants (R', t, fx fy cx cy) in LDS: every
     // candidate reads its reference camera's 16 values there instead of by
-    // per-lane global loads
-    __shared__ double s_cam[MVS_MAX_VIEWS][16];
+    // per-lane global loads.  Field-major ([value][view]): the lanes of a
+    // read (one value of 64 random views) fall in distinct banks; view-major
+    // rows of 128 B put them all in two banks (81 % of k_bin's LDS cycles
+    // were bank conflicts, profiles/r06/pmc_r6e_w5_scorer.csv)
+    __shared__ double s_cam[16][MVS_MAX_VIEWS];
     const int words = (sc.V + 63) >> 6;
     for (int k = threadIdx.x; k < sc.V * 16; k += blockDim.x) {
         const int v = k >> 4, f = k & 15;
         const CamDev& cm = sc.cams[v];
-        s_cam[v][f] = f < 9 ? cm.Rp[f] : f < 12 ? cm.t[f - 9] : f == 12 ? cm.fx : f == 13 ? cm.fy : f == 14 ? cm.cx : cm.cy;
+        s_cam[f][v] = f < 9 ? cm.Rp[f] : f < 12 ? cm.t[f - 9] : f == 12 ? cm.fx : f == 13 ? cm.fy : f == 14 ? cm.cx : cm.cy;
     }
     STAMP(t0);
     if (LDSHIST)
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         const int R = Rk[k];
         const double c[3] = {ck[k][0], ck[k][1], ck[k][2]};
         double px, py;
-        project_vals(s_cam[R], c, px, py);
+        project_vals([&](int f) { return s_cam[f][R]; }, c, px, py);
         a.xy[2 * i] = px;
         a.xy[2 * i + 1] = py;
         int q, r;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-end set on one box: GPU tests, smoke(), the default bench line (its
-# roofline from profiles/r03/pmc.json), then the N=2 exchange rehearsal
+# roofline from the newest profiles/rNN/pmc.json), then the N=2 exchange rehearsal
 # (two ranks on cuda:0 over gloo).  TAG names the outputs.
 export TMPDIR=/tmp
 cd "$(dirname "$0")/.." || exit 1

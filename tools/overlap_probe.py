@@ -33,7 +33,7 @@ PKG_NAME = bench.PKG_NAME
 def cu_mask_stream(torch, dev, ncu, free, order):
     """A stream whose kernels run on ncu - free CUs only (bit k = CU k of the
     mask as HIP numbers them); returns (torch ExternalStream, raw handle)."""
-    hip = ctypes.CDLL("libamdhip64.so")
+    hip = importlib.import_module(PKG_NAME + ".parallel")._hip()   # the runtime torch loaded
     bits = [1] * ncu
     if order == "lo":
         off = list(range(free))
