@@ -381,7 +381,8 @@ struct mvs_ctx {
         }
         return true;
     }
-    int tiles_clean_ntiles = -1;   // tile counters known zero for this tile count (-1: unknown)
+    int tiles_clean_ntiles = -1;   // the next batch's counter set known zero for this tile count (-1: unknown)
+    int tiles_parity = 0;          // the counter set the next tiled batch uses
     // kernel timing (mvs_kernel_timing): one event pair per `timing_period`-th
     // scoring launch (an event record between two kernels costs a few us of
     // stream time, so a timed loop samples)
@@ -549,7 +550,8 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.nty = (ctx->H + MVS_TILE_H - 1) / MVS_TILE_H;
         const int ntiles = t.ntx * t.nty;
         const int32_t* tiles_before = ctx->t_tiles.p;
-        ctx->t_tiles.ensure((size_t)tc_words(ntiles));
+        const int64_t set_words = tc_words(ntiles);
+        ctx->t_tiles.ensure((size_t)(2 * set_words));   // two counter sets (parities)
         if (ctx->t_tiles.p != tiles_before) ctx->tiles_clean_ntiles = -1;
         const int groups = grouped ? (ctx->V + MVS_GROUP_VIEWS - 1) / MVS_GROUP_VIEWS : 1;
         // tile buckets of cap candidates (16x the mean load, at least 1024:
@@ -566,12 +568,16 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         t.cap = (int)cap;
         t.chunk = grouped ? MVS_GROUP_CHUNK : MVS_MMA_CHUNK;
         t.groups = groups;
-        t.tile_count = ctx->t_tiles.p;
-        int32_t* ctl = ctx->t_tiles.p + (int64_t)ntiles * kTcStride;   // one 128-B line per counter
+        // this batch's counter set; k_bin zeroes the other (the previous
+        // batch's) for the next batch
+        int32_t* set = ctx->t_tiles.p + ctx->tiles_parity * set_words;
+        t.tile_count = set;
+        int32_t* ctl = set + (int64_t)ntiles * kTcStride;   // one 128-B line per counter
         t.head = ctl;
         t.fix_count = ctl + 32;
-        t.done = ctl + 64;
         t.n_items = ctl + 96;
+        t.zero_blk = ctx->t_tiles.p + (1 - ctx->tiles_parity) * set_words;
+        t.zero_words = set_words;
         t.sorted = (int2*)ctx->t_cand.p;
         t.fix_list = (int4*)(ctx->t_cand.p + 2 * (size_t)ntiles * cap);
         // at most one partial chunk per tile beyond the full ones, in any one
@@ -592,7 +598,8 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         if (rc != 0) throw Fail{rc == -3 ? MVS_E_UNSUPPORTED : MVS_E_HIP, "tiled score launch failed"};
         ctx->scratch_release(s);
         if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, tab && !grouped ? 2 : 1);
-        ctx->tiles_clean_ntiles = ntiles;        // k_score_fix leaves the counters zero
+        ctx->tiles_clean_ntiles = ntiles;        // the next batch's set was zeroed by this k_bin
+        ctx->tiles_parity ^= 1;
         return;
     }
     hipEvent_t e0, e1;

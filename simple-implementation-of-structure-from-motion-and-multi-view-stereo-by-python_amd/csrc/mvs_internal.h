@@ -80,8 +80,11 @@ struct ScoreArgs {
 #endif
 constexpr int kTcStride = MVS_TC_STRIDE;
 constexpr int kItemSegs = 8;   // k_bin appends work items to 8 segments (workgroup b to segment b % 8)
-// counts, then the control block: head, fix_count, done, the 8 segments' item counts
-inline int64_t tc_words(int ntiles) { return (int64_t)ntiles * kTcStride + (3 + kItemSegs) * 32; }
+constexpr int kBandHeads = 8;   // the tiled scorers' band queue heads (one band per XCD)
+// one counter set: the tile counts, then the control block: head, fix_count,
+// a spare line, the 8 segments' item counts, the band heads (one 128-B line
+// each).  Two sets (parities) alternate between batches.
+inline int64_t tc_words(int ntiles) { return (int64_t)ntiles * kTcStride + (3 + kItemSegs + kBandHeads) * 32; }
 
 // The per-scene moment tables hold D = n S_bb - S_b^2 (int32) where the
 // scorer is k_score_mma_v (V > 64) and w = 1/sqrt(D) (binary64, k_score_tab)
@@ -100,13 +103,16 @@ struct TiledArgs {
     int32_t* fix_count;
     int32_t* n_items;          // kItemSegs counters, 32 ints apart: items in each segment
     int item_seg;              // capacity of a segment (items of segment x at x * item_seg)
-    int32_t* done;
+    // the other parity's counter set (tile counts + control block,
+    // zero_words ints): the previous batch's, zeroed by this batch's k_bin
+    // for the next one
+    int32_t* zero_blk;
+    int64_t zero_words;
     // view groups of 64 (V > 64: k_score_mma_v scores each work item against
     // every group in turn); groups = 1 otherwise
     int groups;
-    // k_score_fix leaves every counter zero for the next batch; zero_first = 1
-    // asks the launcher to clear them first (new scratch, or a previous
-    // sequence that did not complete)
+    // zero_first = 1 asks the launcher to clear both counter sets first (new
+    // scratch, or a previous sequence that did not complete)
     int zero_first;
     int4* items;
     // workgroups of the persistent scorer (0: its default, every CU; fewer

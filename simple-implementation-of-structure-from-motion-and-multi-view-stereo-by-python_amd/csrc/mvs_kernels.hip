@@ -486,6 +486,10 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         s_cam[f][v] = f < 9 ? cm.Rp[f] : f < 12 ? cm.t[f - 9] : f == 12 ? cm.fx : f == 13 ? cm.fy : f == 14 ? cm.cx : cm.cy;
     }
     STAMP(t0);
+    // the previous batch's counter set (the other parity; its k_score_fix
+    // has finished, stream order) back to zero for the batch after this one
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < t.zero_words; k += (int64_t)gridDim.x * blockDim.x)
+        t.zero_blk[k] = 0;
     if (LDSHIST)
         for (int b = threadIdx.x; b < t.ntiles; b += blockDim.x) hist[b] = 0;
     __syncthreads();
@@ -499,6 +503,11 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     const uint16_t* __restrict__ flat = mt.flat;
     int fk[kBinPer];
     int qk[kBinPer], rk[kBinPer];
+    auto settle = [&](int64_t i) {   // V = [], avg 0
+        for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
+        if (a.count) a.count[i] = 0;
+        if (a.avg) a.avg[i * a.astride] = 0.0;
+    };
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
@@ -513,9 +522,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         a.xy[2 * i + 1] = py;
         int q, r;
         if (!window_ok(sc, px, py, wid, &q, &r)) {
-            for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
-            if (a.count) a.count[i] = 0;
-            if (a.avg) a.avg[i * a.astride] = 0.0;
+            settle(i);
             continue;
         }
         tl[k] = 0;
@@ -529,9 +536,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
         if ((fk[k] >> (Rk[k] & 15)) & 1) {
             tl[k] = -1;
-            for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
-            if (a.count) a.count[i] = 0;
-            if (a.avg) a.avg[i * a.astride] = 0.0;
+            settle(i);
             continue;
         }
         const int R = Rk[k], q = qk[k], r = rk[k];
@@ -583,16 +588,23 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     }
     STAMP(t2);
     // straight into the tile's bucket (no separate scatter pass); past the
-    // bucket's capacity to the direct path's list
+    // bucket's capacity to the direct path's list (counted: mvs_scorer_stats)
+    int over = 0;
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
         if (tl[k] < 0) continue;
         const int rank = (LDSHIST ? hist[tl[k]] : 0) + lr[k];
-        if (rank < t.cap)
+        if (rank < t.cap) {
             t.sorted[(int64_t)tl[k] * t.cap + rank] = make_int2((int32_t)i, pk[k]);
-        else
+        } else {
             t.fix_list[atomicAdd(t.fix_count, 1)] = make_int4((int32_t)i, tl[k], pk[k], 0);
+            ++over;
+        }
+    }
+    if (t.stats && __ballot(over != 0)) {
+        over = wave_reduce_add(over);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&t.stats[1], (unsigned long long)over);
     }
     STAMP(t3);
     STAMP_ADD_ROW(2048 + blockIdx.x, 0, 1);
@@ -1481,8 +1493,18 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
                                              4, 0, 0);
     };
 
+    // the items in contiguous bands of tiles, band x claimed first by the
+    // workgroups b = x mod kBandHeads (one band per XCD under round-robin
+    // dispatch: an XCD's workgroups in flight take neighbouring tiles and
+    // share their regions' lines in its L2; ring256 0.498 vs 0.506 ms with
+    // one queue, profiles/r06/r6n_*)
+    const int ob = (int)blockIdx.x % kBandHeads;
+    int cb = ob;   // thread 0's current band
+    auto claim_item = [&]() -> int {
+        return band_claim(head + (3 + kItemSegs) * 32, cb, ob, kBandHeads, n_items, [](int) { return 0; });
+    };
     // the first item: its candidates and group 0's region; the indicator rows
-    if (tid == 0) s_item = atomicAdd(head, 1);
+    if (tid == 0) s_item = claim_item();
     if (tid < 16 * 8) {   // indicator row q: bytes [q + C0, q + C0 + NB) are 1
         const int q = tid >> 3, j = tid & 7;
         const uint32_t wm = ((1u << NB) - 1u) << (q + C0);
@@ -1597,7 +1619,7 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
             // (claimed inside the group loop: a VGPR loaded before the loop and
             // read in it would make the compiler drain every load at loop entry)
             int claim = 0;
-            if (g == 0 && tid == 0) claim = atomicAdd(head, 1);
+            if (g == 0 && tid == 0) claim = claim_item();
             // ---- 2. Q = S_bb of every (pixel, view) of the group ----
             // (TAB: none, the scene's tables hold S_b and D)
             if (TAB) {
@@ -1868,12 +1890,13 @@ __global__ __launch_bounds__(kMmaThreads) void k_score_mma_v(const SceneDev sc, 
     }
 }
 
-// Guard-band candidates of the tiled scorer, re-scored whole by the direct
-// path (whose own guard band leads to the numpy-order ctNcc).  Last kernel of
-// a batch: it leaves the counters zero for the next one (the tile counts by
-// a grid-stride pass; the list's count, the item count and the queue head by
-// the workgroup that finishes last, after every workgroup has read them).
-// The grid has kFixBase workgroups plus, for large batches, more that take
+// Guard-band candidates of the tiled scorer and bucket overflow, re-scored
+// whole by the direct path (whose own guard band leads to the numpy-order
+// ctNcc).  Last kernel of a batch.  It zeroes nothing: the tile counters and
+// the control block come in two parity sets, and the next batch's k_bin
+// zeroes this batch's set (no done ticket here: a kernel with a short list
+// is a launch and one load: 6.8 -> 4.7 us with 30 guard-band entries,
+// profiles/r06/r6p_*).  The grid has kFixBase workgroups plus, for large batches, more that take
 // part only when the list is long (a skewed batch whose tiles overflow their
 // buckets): a guard-band list of a few hundred entries costs no extra
 // workgroups' atomics, a long overflow list gets up to 4x the workgroups.
@@ -1883,19 +1906,12 @@ template <int WID, int NS>
 __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const ScoreArgs a,
                                                    const TiledArgs t) {
     const int nfix = *t.fix_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && t.stats) {
+        t.stats[0] += (unsigned long long)nfix;
+        t.stats[2] += 1ull;
+    }
     const int active = nfix > kFixSmall ? (int)gridDim.x : kFixBase;   // uniform over the grid
     if ((int)blockIdx.x >= active) return;
-    // the tile counters back to zero; the bucket overflow (candidates past a
-    // tile's cap, which k_bin put on the list) counted on the way
-    int over = 0;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < t.ntiles; k += active * 256) {
-        over += max(t.tile_count[k * kTcStride] - t.cap, 0);
-        t.tile_count[k * kTcStride] = 0;
-    }
-    if (t.stats && __syncthreads_or(over != 0)) {
-        over = wave_reduce_add(over);
-        if ((threadIdx.x & 63) == 0 && over) atomicAdd(&t.stats[1], (unsigned long long)over);
-    }
     for (int k = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < nfix;
          k += active * 4) {
         const int4 f = t.fix_list[k];
@@ -1906,17 +1922,6 @@ __global__ __launch_bounds__(256) void k_score_fix(const SceneDev sc, const Scor
         const int q = tx * MVS_TILE_W + (pk & 15), r = ty * MVS_TILE_H + ((pk >> 4) & 7), R = pk >> 7;
         wave_score<WID, NS>(sc, R, q, r, a.thr, a.mask + cand * a.mstride, a.count ? a.count + cand : nullptr,
                             a.avg ? a.avg + cand * a.astride : nullptr, a.exact_hits);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(t.done, 1) == active - 1) {
-        if (t.stats) {
-            t.stats[0] += (unsigned long long)nfix;
-            t.stats[2] += 1ull;
-        }
-        *t.fix_count = 0;
-        for (int x = 0; x < kItemSegs; ++x) t.n_items[32 * x] = 0;
-        *t.head = 0;
-        *t.done = 0;
     }
 }
 
@@ -2143,6 +2148,24 @@ typedef acc_l2v acc_l2 __attribute__((aligned(8)));
 static_assert(kAccChunk == MVS_ACC_CHUNK, "the host sizes the pack's grid by MVS_ACC_CHUNK");
 static_assert(kAccE <= 128, "wave 0 scans at most two (j, wave) counts per lane");
 
+// a chunk's ticket, taken after its reservation (base) has returned; the last
+// one writes the header and returns the counter and the ticket to zero
+DEV void acc_ticket(unsigned long long* __restrict__ ctl, unsigned long long base, int64_t nch, int64_t n, int width,
+                    int64_t* __restrict__ out) {
+    // the ticket's address depends on the reservation's result (always 0 +
+    // 16; opaque to the compiler), so it issues after the return
+    const int dep = opaque((int)(base >> 63));
+    const unsigned long long tk = atomicAdd(&ctl[16 + dep], 1ull);
+    if ((int64_t)tk == nch - 1) {
+        const int64_t total = (int64_t)__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        out[0] = total;
+        out[1] = n;
+        for (int q = 2; q < width; ++q) out[q] = 0;
+        __hip_atomic_store(&ctl[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctl[16], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ctl: [0] the row counter, [16] the chunk ticket (128 B apart), both zero
 // between calls
 __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t offset, const int32_t* __restrict__ count,
@@ -2224,22 +2247,13 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
             // returned: the last ticket sees every chunk's rows counted)
             const unsigned long long base = T ? atomicAdd(&ctl[0], T) : 0ull;
             s_base = (int64_t)base;
-            // the ticket's address depends on the reservation's result (always
-            // 0 + 16; opaque to the compiler), so it issues after the return
-            const int dep = opaque((int)(base >> 63));
-            const unsigned long long tk = atomicAdd(&ctl[16 + dep], 1ull);
-            if ((int64_t)tk == nch - 1) {
-                const int64_t total = (int64_t)__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                out[0] = total;
-                out[1] = n;
-                for (int q = 2; q < width; ++q) out[q] = 0;
-                __hip_atomic_store(&ctl[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&ctl[16], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
         }
     }
     lds_barrier();
     const int64_t base = s_base;
+    // the ticket is taken here, off the rows' critical path (11.07 vs 11.43
+    // us with the ticket before the barrier, profiles/r06/r6m_*)
+    if (threadIdx.x == 0) acc_ticket(ctl, (unsigned long long)base, nch, n, width, out);
 #pragma unroll
     for (int j = 0; j < kAccPer; ++j) {
         if ((m[j] >> lane) & 1ull) {
@@ -2464,10 +2478,12 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
         t->chunk != (grouped ? kGroupChunk : kMmaChunk) || t->groups != (grouped ? (sc->V + 63) / 64 : 1) ||
         sc->V > MVS_MAX_VIEWS)
         return -3;
-    // tile counters and the control block (queue head, fix_count, n_items,
-    // done): left at zero by the previous batch's k_score_fix unless zero_first
+    // tile counters and the control block (queue heads, fix_count, n_items)
+    // of this parity: zeroed by the previous batch's k_bin, unless
+    // zero_first (both sets)
     if (t->zero_first &&
-        hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * tc_words(t->ntiles), s) != hipSuccess)
+        (hipMemsetAsync(t->tile_count, 0, sizeof(int32_t) * tc_words(t->ntiles), s) != hipSuccess ||
+         hipMemsetAsync(t->zero_blk, 0, sizeof(int32_t) * t->zero_words, s) != hipSuccess))
         return -1;
     const int64_t per_block = (int64_t)kBinBlock * kBinPer;
     const int nbin = (int)((a->n + per_block - 1) / per_block);

@@ -59,6 +59,21 @@ DEV int opaque(int x) {
     return x;
 }
 
+// Band queues of a persistent scorer: work items [0, n) in nb contiguous
+// bands, band x's head at heads[32 x]; the first skip(x) items of band x are
+// handed out without a claim.  A workgroup claims from band cb (its own band
+// first) and moves to the next band when that one is exhausted; n: none left.
+template <class Skip>
+DEV int band_claim(int32_t* heads, int& cb, int ob, int nb, int n, Skip&& skip) {
+    for (; cb < ob + nb; ++cb) {
+        const int x = cb % nb;
+        const int lo = (int)((int64_t)n * x / nb), hi = (int)((int64_t)n * (x + 1) / nb);
+        const int r = atomicAdd(heads + 32 * x, 1) + skip(x);
+        if (r < hi - lo) return lo + r;
+    }
+    return n;
+}
+
 // acc += num * w in the lanes of P only (binary64): EXEC narrowed to P for
 // the conversion and the fma, restored after -- two vector instructions, no
 // select of the term (the compiler's form of the select costs four)

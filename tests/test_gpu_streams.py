@@ -211,3 +211,60 @@ def test_points_exchange_pack_on_comm_world1(pkg, ctx, dino):
     par.pack_accepted_reference(3000, None, prev_rec, 3, exp, torch.from_numpy(sweeps[3][0]))
     got, acc = blk[0].cpu(), int(exp[0, 0])
     assert torch.equal(got[0], exp[0]) and torch.equal(par.sort_rows(got[1:1 + acc]), exp[1:1 + acc])
+
+
+def _skewed_candidates(n, K, R, t, seed):
+    """n candidates crowded onto two pixel tiles (most overflow the buckets)."""
+    rng = np.random.default_rng(seed)
+    ref = rng.integers(0, 48, n).astype(np.int32)
+    x = np.where(rng.random(n) < 0.5, 300.0, 333.0) + rng.random(n) * 15.9
+    y = 200 + rng.random(n) * 7.9
+    z = rng.uniform(0.6, 0.72, n)
+    Kinv = np.linalg.inv(K)
+    ray = np.einsum("nij,nj->ni", Kinv[ref], np.stack([x, y, np.ones(n)], 1))
+    c = np.einsum("nji,nj->ni", R[ref], z[:, None] * ray - t[ref].reshape(n, 3))
+    return np.ascontiguousarray(c), ref
+
+
+def test_counter_sets_alternate_across_batch_kinds(pkg, dino, oracle_scene):
+    """The tiled scorer's two counter sets (parities): each batch's k_bin
+    zeroes the previous batch's set, so no kernel after the scorer zeroes
+    anything.  A fresh context runs, on two streams in turn, a skewed batch
+    (bucket overflow onto the direct path's list), a dense batch (implicit
+    items), a sparse one (k_item_scan), a small one (the direct kernel: no
+    counters touched) and the dense and skewed ones again: every output
+    equals the oracle's, and the statistics count the overflow of the skewed
+    batches only."""
+    import torch
+    rgb, K, R, t = dino
+    dev = torch.device("cuda:0")
+    batches = {
+        "skewed": _skewed_candidates(1 << 15, K, R, t, seed=51),
+        "dense": bench_candidates(1 << 18, K, R, t, seed=52),
+        "sparse": bench_candidates(50000, K, R, t, seed=53),
+        "small": bench_candidates(1500, K, R, t, seed=54),
+    }
+    want = {k: oracle_scene.score_batch(c, ref, 0.7, 5, nthreads=16) for k, (c, ref) in batches.items()}
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    with pkg.MvsContext(rgb, K, R, t, device=0) as cx:
+        overflow = {}
+        for j, kind in enumerate(["skewed", "dense", "sparse", "small", "dense", "skewed", "sparse"]):
+            c, ref = batches[kind]
+            n = len(ref)
+            tc, tr = torch.from_numpy(c).to(dev), torch.from_numpy(ref).to(dev)
+            xy = torch.empty((n, 2), dtype=torch.float64, device=dev)
+            rec = torch.full((n, 2), -1, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            before = cx.scorer_stats()
+            s = streams[j % 2]
+            cx.score_device_rec(tc, tr, xy, rec, 0.7, 5, stream=s.cuda_stream)
+            s.synchronize()
+            after = cx.scorer_stats()
+            oxy, omask, ocount, oavg = want[kind]
+            m, cnt = _outputs(rec)
+            assert np.array_equal(m, omask[:, 0]) and np.array_equal(cnt, ocount), (j, kind)
+            assert np.allclose(rec.cpu().numpy()[:, 1].view(np.float64), oavg, rtol=0, atol=1e-12), (j, kind)
+            assert np.array_equal(xy.cpu().numpy(), oxy), (j, kind)
+            overflow.setdefault(kind, []).append(after["overflow"] - before["overflow"])
+        assert all(v > 0 for v in overflow["skewed"]) and overflow["skewed"][0] == overflow["skewed"][1]
+        assert overflow["dense"] == [0, 0] and overflow["sparse"] == [0, 0] and overflow["small"] == [0]

@@ -30,7 +30,7 @@ for v in main ${VARIANTS}; do
   f=$(find gpurun_out/prof_$S -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/${S}_kernel_stats.csv
   rm -rf gpurun_out/prof_$S
   echo "== $v (rocprof)" | tee -a gpurun_out/${T}_ab.log
-  python tools/ksumm.py gpurun_out/${S}_kernel_stats.csv | head -8 | tee -a gpurun_out/${T}_ab.log
+  python tools/ksumm.py gpurun_out/${S}_kernel_stats.csv 8 | tee -a gpurun_out/${T}_ab.log
 done
 fi
 if [ -n "$EXTRA" ]; then bash -c "$EXTRA" || exit 1; fi
