@@ -503,38 +503,55 @@ __global__ __launch_bounds__(kBinBlock) void k_bin(const SceneDev sc, const Scor
     const uint16_t* __restrict__ flat = mt.flat;
     int fk[kBinPer];
     int qk[kBinPer], rk[kBinPer];
-    auto settle = [&](int64_t i) {   // V = [], avg 0
-        for (int w = 0; w < words; ++w) a.mask[i * a.mstride + w] = 0;
+    // V = [], avg 0.  Records (a.rec, V <= 64): one 16-B store.  No loop
+    // with a run-time trip count here: the compiler's wait-count tracking
+    // then stays exact, where a loop made it wait for every store of the
+    // thread (vmcnt(0)) before the first (workgroup, tile) atomic
+    auto settle = [&](int64_t i) {
+        if (a.rec && words == 1) {
+            *(uint4*)(a.mask + 2 * i) = make_uint4(0u, 0u, 0u, 0u);
+            return;
+        }
+#pragma unroll
+        for (int w = 0; w < MVS_MAX_VIEWS / 64; ++w)
+            if (w < words) a.mask[i * a.mstride + w] = 0;
         if (a.count) a.count[i] = 0;
         if (a.avg) a.avg[i * a.astride] = 0.0;
     };
+    // Every load of these two loops is issued and consumed on every path
+    // (past the batch: candidate 0's values; invalid window: pixel (0, 0)'s
+    // bits), so that no path leaves a load pending at the loops' joins: the
+    // compiler's wait counting then stays exact, where a conditionally
+    // consumed load made it wait for every memory operation of the thread
+    // (vmcnt(0): the xy and settled stores included) ahead of the barrier
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        tl[k] = -1;
-        fk[k] = 0;
-        if (i >= a.n) continue;
         const int R = Rk[k];
         const double c[3] = {ck[k][0], ck[k][1], ck[k][2]};
         double px, py;
         project_vals([&](int f) { return s_cam[f][R]; }, c, px, py);
-        a.xy[2 * i] = px;
-        a.xy[2 * i + 1] = py;
-        int q, r;
-        if (!window_ok(sc, px, py, wid, &q, &r)) {
-            settle(i);
-            continue;
-        }
-        tl[k] = 0;
+        int q = 0, r = 0;
+        const bool inb = i < a.n, ok = inb && window_ok(sc, px, py, wid, &q, &r);
+        if (!ok) q = r = 0;
+        tl[k] = ok ? 0 : inb ? -1 : -2;   // -2: past the batch
         qk[k] = q;
         rk[k] = r;
-        if (flat) fk[k] = flat[((int64_t)r * sc.W + q) * (mt.VP >> 4) + (R >> 4)];
+        // the stores ahead of the bit load: the wait for the last load then
+        // waits for nothing behind it
+        if (inb) {
+            a.xy[2 * i] = px;
+            a.xy[2 * i + 1] = py;
+        }
+        if (inb && !ok) settle(i);
+        fk[k] = flat ? flat[((int64_t)r * sc.W + q) * (mt.VP >> 4) + (R >> 4)] : 0;
     }
 #pragma unroll
     for (int k = 0; k < kBinPer; ++k) {
+        const bool cst = (fk[k] >> (Rk[k] & 15)) & 1;
         if (tl[k] < 0) continue;
         const int64_t i = base + (int64_t)k * kBinBlock + threadIdx.x;
-        if ((fk[k] >> (Rk[k] & 15)) & 1) {
+        if (cst) {
             tl[k] = -1;
             settle(i);
             continue;

@@ -303,14 +303,13 @@ __global__ __launch_bounds__(kTabThreads, kTabMinWaves) void k_score_tab(const S
         return make_int4(tile, tile * t.cap + j * t.chunk, min(min(c, t.cap) - j * t.chunk, t.chunk),
                          min(t.chunk, t.cap - j * t.chunk));
     };
-    // vector loads (a lane-dependent-looking address): their wait is the
-    // in-order vmcnt at the round's end, not lgkmcnt(0) in front of every LDS
-    // read of the round
+    // an item's (tile, chunk): implicit items below ntiles are computed (no
+    // load: the round's DMA issue then waits for nothing; the load and the
+    // select of round 5 made every wave wait a memory round trip there);
+    // else a vector load (a lane-dependent-looking address)
     auto item_v = [&](int v) -> int2 {
-        // the load is issued either way (its wait stays the round end's vmcnt)
-        const int2 ld = *(const int2*)(items + opaque(implicit ? t.item_seg + max(v - t.ntiles, 0) : im.slot(v)));
         if (implicit && v < t.ntiles) return make_int2(v, 0);
-        return ld;
+        return *(const int2*)(items + opaque(implicit ? t.item_seg + max(v - t.ntiles, 0) : im.slot(v)));
     };
     auto count_v = [&](int tile) -> int { return t.tile_count[opaque(tile * kTcStride)]; };
     // the item pipeline: while item k is scored, item k+1's region and list
