@@ -2202,6 +2202,7 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
     // counts (records: popcounts of the words)
     uint64_t m[kAccPer], w0[kAccPer];
     int c[kAccPer];
+    double px[kAccPer], py[kAccPer], pz[kAccPer];
 #pragma unroll
     for (int j = 0; j < kAccPer; ++j) {
         const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
@@ -2218,7 +2219,6 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
     }
     // the accepted candidates' points, in flight across the scan and the
     // reservation (LDS-only barriers)
-    double px[kAccPer], py[kAccPer], pz[kAccPer];
 #pragma unroll
     for (int j = 0; j < kAccPer; ++j) {
         const int64_t i = b * kAccChunk + j * kAccThreads + threadIdx.x;
@@ -2226,6 +2226,9 @@ __global__ __launch_bounds__(kAccThreads) void k_acc_pack(int64_t n, int64_t off
         m[j] = __ballot(acc);
         px[j] = py[j] = pz[j] = 0.0;
         if (cpt && acc) {
+            // (every candidate's point loaded with the mask words instead --
+            // coalesced, but 25 MB instead of the accepted ones' 6 MB:
+            // 12.26 vs 11.18 us, profiles/r06/r6u_*)
             // x, y as one 16-B load (8-B aligned), z beside it
             const acc_d2 xy = *(const acc_d2*)(cpt + 3 * i);
             px[j] = xy.x;
