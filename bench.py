@@ -417,9 +417,6 @@ def main():
     ap.add_argument("--pack-on-comm", action="store_true",
                     help="N > 1: pack on the exchange's stream (the CUs the masked scoring stream leaves "
                          "out), overlapping the next sweep (default: on the scoring stream, after the sweep)")
-    ap.add_argument("--pipeline", type=int, choices=[0, 1], default=0,
-                    help="1: two paired contexts score alternate sweeps on two streams (mvs_pair_scorers: "
-                         "a sweep's k_bin beside the previous sweep's scorer, the scorers one at a time)")
     ap.add_argument("--scene", choices=["dino", "ring256"], default="dino",
                     help="headline scene (ring256: config 4 as the headline, for profiling)")
     argv = json.loads(os.environ["MVS_BENCH_ARGV"]) if "MVS_BENCH_ARGV" in os.environ else None
@@ -430,8 +427,6 @@ def main():
         # the SoA outputs are single-buffered: the next sweep would overwrite
         # count / mask while the comm stream's pack still reads them
         raise SystemExit("--pack-on-comm needs the record outputs (not --soa)")
-    if a.pipeline and a.pack_on_comm:
-        raise SystemExit("--pipeline scores on two streams; --pack-on-comm assumes one")
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # no launcher: this process starts the ranks and never touches the GPU
         sys.exit(launch_ranks(a.gpus))
@@ -500,21 +495,15 @@ def main():
                 "rec": None if a.soa else torch.empty((n, (ctx_V + 63) // 64 + 1), dtype=torch.int64, device=dev),
                 "avg": torch.empty(n, dtype=torch.float64, device=dev)}
 
-    def timed(cx, sw, wid, steps, warmup, exchange=True, rebuild=False, st=None, pipe=None):
+    def timed(cx, sw, wid, steps, warmup, exchange=True, rebuild=False, st=None):
         """steps timed sweeps on stream st (default: the scoring stream) ->
         (wall s (max over ranks), kernel ms per launch, score-call ms, records
-        exchanged in the last step).  pipe = (context, stream, outputs) of a
-        second lane paired with cx (--pipeline): sweep k on lane k % 2."""
+        exchanged in the last step)."""
         got = {"n": 0}
         st = st or stream
         ex = sw.get("exch") if exchange else None
-        lanes = [(cx, st, sw)] + ([pipe] if pipe is not None else [])
-        cur = {"k": 0}
 
         def step(evs=None):
-            nonlocal cx, st, sw
-            cx, st, sw = lanes[cur["k"] % len(lanes)]
-            cur["k"] += 1
             rec = None
             if ex is not None and ex.pack_on_comm and sw["rec"] is not None:
                 # two record buffers: sweep k+1 scores into one while the comm
@@ -549,11 +538,7 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        cur["k"] = 0
-        for lx, _, _ in lanes:
-            # HIP events around the dominant kernel, on its stream (a lane's
-            # every TIME_EVERY-th call: the same sample of steps)
-            lx.kernel_timing(True, every=max(TIME_EVERY // len(lanes), 1))
+        cx.kernel_timing(True, every=TIME_EVERY)   # HIP events around the dominant kernel, on its stream
         t0 = time.perf_counter()
         for k in range(steps):
             step(evs.get(k))
@@ -561,13 +546,9 @@ def main():
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        kt, kl = 0.0, 0
-        for lx, _, _ in lanes:
-            lx.kernel_timing(False)
-            t_, l_ = lx.kernel_time()
-            kt, kl = kt + t_, kl + l_
-        cx, st, sw = lanes[0]
-        if kl < len(timed_steps) or kt <= 0.0:
+        cx.kernel_timing(False)
+        kt, kl = cx.kernel_time()
+        if kl != len(timed_steps) or kt <= 0.0:
             raise RuntimeError(f"kernel timing recorded {kl} launches / {kt} ms for {len(timed_steps)} timed steps")
         pms = sum(e0.elapsed_time(e1) for e0, e1 in evs.values()) / len(evs)
         if ex is not None:
@@ -598,28 +579,8 @@ def main():
         else:
             kept = torch.cuda.get_device_properties(dev).multi_processor_count - a.comm_cus
 
-    # --pipeline: a second context of the scene paired with ctx (its scorer
-    # and ctx's take turns; each lane's binning may overlap the other's
-    # scorer), its own stream and output buffers, the same inputs
-    pipe, pipe_owner = None, None
-    if a.pipeline:
-        ctx2 = pkg.MvsContext(rgb, K, R, t, device=local)
-        ctx.pair_scorers(ctx2)
-        if a.comm_cus > 0 and a.comm_layout == "mask" and (world > 1 or rank == 0):
-            pipe_owner = par.cu_masked_stream(dev, a.comm_cus)
-            owners.append(pipe_owner)
-        stream2 = pipe_owner.stream if pipe_owner is not None else torch.cuda.Stream(dev)
-        sw2 = dict(sw)
-        for key in ("xy", "mask", "count", "rec", "avg"):
-            if sw2[key] is not None:
-                sw2[key] = torch.empty_like(sw[key])
-        sw2.pop("recs", None)
-        pipe = (ctx2, stream2, sw2)
-
     def masked(on):
         ctx.set_scorer_grid(2 * kept if on and kept else 0)
-        if pipe is not None:
-            pipe[0].set_scorer_grid(2 * kept if on and kept else 0)
 
     pack_on_comm = a.pack_on_comm
     if world > 1:
@@ -635,8 +596,7 @@ def main():
         masked(True)
     total_n = a.n if a.strong else a.n * world
     st0 = scorer_stats(ctx)
-    dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream if world > 1 else stream,
-                                   pipe=pipe)
+    dt, kms, pms, gathered = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream if world > 1 else stream)
     direct = direct_path(st0, scorer_stats(ctx))
     masked(False)
     value = total_n * a.steps / dt
@@ -656,7 +616,7 @@ def main():
         sw["exch"] = par.PointsExchange(ctx, (V + 63) // 64, cap1, dev, pack_on_comm=pack_on_comm,
                                         comm_stream=cowner if pack_on_comm else None)
         masked(True)
-        pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream, pipe=pipe)
+        pdt, _, _, packed = timed(ctx, sw, a.wid, a.steps, a.warmup, st=mstream)
         masked(False)
         del sw["exch"]
         if packed != accepted:
@@ -715,9 +675,6 @@ def main():
         "direct_path": direct,
         "exchange": exchange_figures(ctx, sw, V, vlb, accepted, world, stream, a.thr, a.wid),
     }
-    out["pipeline"] = (("two paired contexts on two streams, alternate sweeps: a sweep's k_bin may overlap the "
-                        "previous sweep's scorer; the scorers run one at a time (mvs_pair_scorers)")
-                       if pipe is not None else None)
     out["roofline"] = roofline(pmc_entry(a.scene, V, a.wid, n, kernel_name), V, a.wid, n, kms, kernel_name,
                                floor_bytes(rgb, sw["xy"], sw["ref"], a.wid, n))
     if solo and not a.no_overlap:
@@ -843,8 +800,6 @@ def main():
         o.close()
     if world > 1:
         dist.destroy_process_group()
-    if pipe is not None:
-        pipe[0].close()
     ctx.close()
 
 

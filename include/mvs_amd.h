@@ -140,13 +140,6 @@ int mvs_proxy_copy(void* d_dst, const void* d_src, int64_t bytes, int workgroups
  * whose CU mask leaves a few CUs to the exchange's pack and RCCL's kernels
  * (parallel.cu_masked_stream); no reference counterpart. */
 int mvs_set_scorer_grid(mvs_ctx* ctx, int workgroups);
-/* Two contexts of one scene on one device that score alternate batches on
- * their own streams (a pipelined sweep queue): each context's tiled scorer
- * waits until the other's last queued batch has finished (the peer's
- * k_score_fix), while its binning (k_bin) may run beside the peer's scorer --
- * on the CUs the persistent scorer's tail leaves idle.  b = NULL unpairs a.
- * Destroying either context unpairs both.  No reference counterpart. */
-int mvs_pair_scorers(mvs_ctx* a, mvs_ctx* b);
 /* Kernel timing (measurement only): while enabled, every enable-th scoring
  * call (enable = 1: every call) records a HIP event pair on its stream
  * immediately around the dominant scoring kernel (k_score_mma / k_score_mma_v

@@ -40,7 +40,6 @@ SIGNATURES = [
     ("mvs_pack_accepted", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int,
                                          ctypes.c_int64, _vp, _vp]),
     ("mvs_set_scorer_grid", ctypes.c_int, [_vp, ctypes.c_int]),
-    ("mvs_pair_scorers", ctypes.c_int, [_vp, _vp]),
     ("mvs_proxy_copy", ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp]),
     ("mvs_filter_outliers", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p,
                                            _u64p, _i32p, _dp, _dp, _dp, _u8p, _i64p]),
@@ -403,14 +402,6 @@ class MvsContext:
         """Hold the persistent scorers to `workgroups` workgroups (0: default,
         two per CU): the grid for a CU-masked scoring stream."""
         check(load().mvs_set_scorer_grid(self._h, int(workgroups)), self._h, "mvs_set_scorer_grid")
-
-    def pair_scorers(self, other=None):
-        """Pipelined sweeps (mvs_pair_scorers): this context and `other` (same
-        scene and device, each scoring on its own stream) alternate batches;
-        a batch's binning may overlap the other context's scorer, the tiled
-        scorers run one at a time.  other=None unpairs."""
-        oh = other._h if other is not None else None
-        check(load().mvs_pair_scorers(self._h, oh), self._h, "mvs_pair_scorers")
 
     def harris_points(self, view):
         """getHarrisPoints(imgs[view]) (HarrisFeatures.py:135-161) on the GPU:

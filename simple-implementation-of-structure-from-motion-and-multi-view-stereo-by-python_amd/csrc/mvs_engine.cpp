@@ -324,11 +324,6 @@ struct mvs_ctx {
     // MVS_SCORE_KERNEL=mma), 2 = tables (env MVS_SCORE_KERNEL=tab)
     int tab_mode = 0;
     int scorer_wgs = 0;   // env MVS_SCORER_WGS: k_score_tab's grid (0 = every CU, twice)
-    // mvs_pair_scorers: the peer context whose tiled scorer this one's waits
-    // for (its last queued batch's k_score_fix, event gate_done), and this
-    // context's own gate_done, recorded after each tiled batch's k_score_fix
-    mvs_ctx* gate_peer = nullptr;
-    hipEvent_t gate_done = nullptr;
     DevBuf<int16_t> mom_sb[MVS_MAX_WID + 1];
     DevBuf<double> mom_w[MVS_MAX_WID + 1];     // V <= 64
     DevBuf<int32_t> mom_d[MVS_MAX_WID + 1];    // V > 64 (moments_dtab)
@@ -599,10 +594,8 @@ void score_device(mvs_ctx* ctx, int64_t n, const double* d_c, const int32_t* d_r
         ctx->scratch_acquire(s);
         const bool tab = ctx->ensure_moments(wid, s);
         const MomentsDev mt = ctx->moments(wid);
-        hipEvent_t gate = ctx->gate_peer ? ctx->gate_peer->gate_done : nullptr;
-        const int rc = mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, tab ? &mt : nullptr, s, e0, e1, gate);
+        const int rc = mvs_launch_score_tiled(&ctx->sc, &a, &t, wid, tab ? &mt : nullptr, s, e0, e1);
         if (rc != 0) throw Fail{rc == -3 ? MVS_E_UNSUPPORTED : MVS_E_HIP, "tiled score launch failed"};
-        if (ctx->gate_done) HIPCHK(hipEventRecord(ctx->gate_done, s));
         ctx->scratch_release(s);
         if (e0) ctx->timed_name = mvs_timed_kernel_name(ctx->V, wid, tab && !grouped ? 2 : 1);
         ctx->tiles_clean_ntiles = ntiles;        // the next batch's set was zeroed by this k_bin
@@ -1450,13 +1443,6 @@ void mvs_ctx_destroy(mvs_ctx* ctx) {
     if (ctx->scratch_order.used || ctx->pack_order.used) (void)hipDeviceSynchronize();
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    if (ctx->gate_peer) ctx->gate_peer->gate_peer = nullptr;
-    if (ctx->gate_done) {
-        // a peer's queued scorer may still wait on it
-        (void)hipEventSynchronize(ctx->gate_done);
-        (void)hipDeviceSynchronize();
-        (void)hipEventDestroy(ctx->gate_done);
-    }
     for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
     if (ctx->scratch_order.ev) (void)hipEventDestroy(ctx->scratch_order.ev);
     if (ctx->pack_order.ev) (void)hipEventDestroy(ctx->pack_order.ev);
@@ -1591,29 +1577,6 @@ int mvs_set_scorer_grid(mvs_ctx* ctx, int workgroups) {
     if (workgroups < 0) return set_err(ctx, Fail{MVS_E_ARG, "workgroups must be >= 0"});
     ctx->scorer_wgs = workgroups;
     return 0;
-}
-
-int mvs_pair_scorers(mvs_ctx* a, mvs_ctx* b) {
-    if (!a) return set_err(nullptr, Fail{MVS_E_ARG, "null context"});
-    if (a == b) return set_err(a, Fail{MVS_E_ARG, "a context cannot pair with itself"});
-    if (b && b->device != a->device) return set_err(a, Fail{MVS_E_ARG, "paired contexts must share a device"});
-    return guarded(a, [&]() {
-        // unpair a (and its old peer), then pair a and b
-        auto unpair = [](mvs_ctx* c) {
-            if (c && c->gate_peer) {
-                c->gate_peer->gate_peer = nullptr;
-                c->gate_peer = nullptr;
-            }
-        };
-        unpair(a);
-        if (!b) return 0;
-        unpair(b);
-        for (mvs_ctx* c : {a, b})
-            if (!c->gate_done) HIPCHK(hipEventCreateWithFlags(&c->gate_done, hipEventDisableTiming));
-        a->gate_peer = b;
-        b->gate_peer = a;
-        return 0;
-    });
 }
 
 int mvs_score(mvs_ctx* ctx, int64_t n, const double* c, const int32_t* ref, int wid, double min_ncc,

@@ -214,11 +214,8 @@ int mvs_launch_score(const SceneDev* sc, const ScoreArgs* a, int wid, hipStream_
                      hipEvent_t ev0, hipEvent_t ev1);
 // tiled scorer: k_bin (tile buckets, then the work items), k_score_mma or k_score_mma_v
 // (timed by ev0/ev1), k_score_fix
-// gate != null: the scorer (after k_bin and k_item_scan) waits on it
-// (mvs_pair_scorers: the peer context's last batch done)
 int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
-                           const MomentsDev* mt, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
-                           hipEvent_t gate = nullptr);
+                           const MomentsDev* mt, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 // the window-moment tables of one wid (mvs_score_tab.hip)
 int mvs_launch_moments(const SceneDev* sc, const MomentsDev* mt, hipStream_t s);
 // k_score_tab (V <= 64, the moments from the tables); k_bin has run

@@ -2491,7 +2491,7 @@ int launch_mma(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const
 
 template <int WID>
 int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, const MomentsDev* mt,
-                         hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t gate) {
+                         hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (a->n == 0) return 0;
     const bool grouped = sc->V > kGroupViews;
     if (t->tw != MVS_TILE_W || t->th != MVS_TILE_H || t->items == nullptr ||
@@ -2522,9 +2522,6 @@ int launch_score_tiled_w(const SceneDev* sc, const ScoreArgs* a, const TiledArgs
     // the work items in tile order (the scorers' workgroups in flight then
     // share image rows -- and at V > 64 table rows -- in L2)
     if (!tv.implicit) hipLaunchKernelGGL(k_item_scan, dim3(1), dim3(kScanThreads), 0, s, tv);
-    // paired contexts: this batch's binning may run beside the peer's scorer,
-    // the scorers themselves one at a time
-    if (gate && hipStreamWaitEvent(s, gate, 0) != hipSuccess) return -1;
     t = &tv;
     int rc = 0;
     {
@@ -2628,13 +2625,13 @@ extern "C" const char* mvs_timed_kernel_name(int V, int wid, int tiled) {
 }
 
 extern "C" int mvs_launch_score_tiled(const SceneDev* sc, const ScoreArgs* a, const TiledArgs* t, int wid,
-                                      const MomentsDev* mt, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t gate) {
+                                      const MomentsDev* mt, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     switch (wid) {
-        case 1: return launch_score_tiled_w<1>(sc, a, t, mt, s, ev0, ev1, gate);
-        case 2: return launch_score_tiled_w<2>(sc, a, t, mt, s, ev0, ev1, gate);
-        case 3: return launch_score_tiled_w<3>(sc, a, t, mt, s, ev0, ev1, gate);
-        case 4: return launch_score_tiled_w<4>(sc, a, t, mt, s, ev0, ev1, gate);
-        case 5: return launch_score_tiled_w<5>(sc, a, t, mt, s, ev0, ev1, gate);
+        case 1: return launch_score_tiled_w<1>(sc, a, t, mt, s, ev0, ev1);
+        case 2: return launch_score_tiled_w<2>(sc, a, t, mt, s, ev0, ev1);
+        case 3: return launch_score_tiled_w<3>(sc, a, t, mt, s, ev0, ev1);
+        case 4: return launch_score_tiled_w<4>(sc, a, t, mt, s, ev0, ev1);
+        case 5: return launch_score_tiled_w<5>(sc, a, t, mt, s, ev0, ev1);
         default: return -2;
     }
 }

@@ -268,49 +268,3 @@ def test_counter_sets_alternate_across_batch_kinds(pkg, dino, oracle_scene):
             overflow.setdefault(kind, []).append(after["overflow"] - before["overflow"])
         assert all(v > 0 for v in overflow["skewed"]) and overflow["skewed"][0] == overflow["skewed"][1]
         assert overflow["dense"] == [0, 0] and overflow["sparse"] == [0, 0] and overflow["small"] == [0]
-
-
-def test_paired_scorers_pipelined_sweeps(pkg, dino, oracle_scene):
-    """mvs_pair_scorers: two contexts of the scene alternate six sweeps on
-    their own streams without any host synchronisation between them (the next
-    sweep's k_bin beside the other context's scorer, the scorers gated one at
-    a time); every sweep's records and projections equal the oracle's.  Then
-    one context is closed (unpairing its peer) and the peer scores alone."""
-    import torch
-    rgb, K, R, t = dino
-    dev = torch.device("cuda:0")
-    n = 1 << 17
-    sweeps = [bench_candidates(n, K, R, t, seed=60 + k) for k in range(3)]
-    want = [oracle_scene.score_batch(c, ref, 0.7, 5, nthreads=16) for c, ref in sweeps]
-    ins = [(torch.from_numpy(c).to(dev), torch.from_numpy(ref).to(dev)) for c, ref in sweeps]
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-    outs = [(torch.empty((n, 2), dtype=torch.float64, device=dev),
-             torch.full((n, 2), -1, dtype=torch.int64, device=dev)) for _ in range(6)]
-    a = pkg.MvsContext(rgb, K, R, t, device=0)
-    b = pkg.MvsContext(rgb, K, R, t, device=0)
-    try:
-        a.pair_scorers(b)
-        torch.cuda.synchronize()
-        for k in range(6):
-            cx, s = (a, b)[k % 2], streams[k % 2]
-            tc, tr = ins[k % 3]
-            cx.score_device_rec(tc, tr, outs[k][0], outs[k][1], 0.7, 5, stream=s.cuda_stream)
-        torch.cuda.synchronize()
-        for k in range(6):
-            oxy, omask, ocount, oavg = want[k % 3]
-            m, cnt = _outputs(outs[k][1])
-            assert np.array_equal(m, omask[:, 0]) and np.array_equal(cnt, ocount), k
-            assert np.allclose(outs[k][1].cpu().numpy()[:, 1].view(np.float64), oavg, rtol=0, atol=1e-12), k
-            assert np.array_equal(outs[k][0].cpu().numpy(), oxy), k
-    finally:
-        b.close()
-    try:
-        xy, rec = outs[0]
-        rec.fill_(-1)
-        torch.cuda.synchronize()
-        a.score_device_rec(*ins[0], xy, rec, 0.7, 5, stream=streams[0].cuda_stream)
-        streams[0].synchronize()
-        m, cnt = _outputs(rec)
-        assert np.array_equal(m, want[0][1][:, 0]) and np.array_equal(cnt, want[0][2])
-    finally:
-        a.close()

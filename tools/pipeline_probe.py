@@ -3,9 +3,7 @@ stream, on the bench's dinoRing 2^20 sweep (records, wid 5).  The question:
 how much of k_bin / k_score_fix / the scorer's tail hides when the next
 sweep's kernels may start on CUs the current sweep's persistent scorer
 leaves idle.  MODE=ctx: two MvsContexts (own scratch each); MODE=lib: one
-context used from two streams (its scratch slots); MODE=gate: two contexts
-paired by mvs_pair_scorers (the next sweep's k_bin beside this sweep's
-scorer, the scorers one at a time).
+context used from two streams (its scratch slots).
 usage: python tools/pipeline_probe.py [steps]"""
 import importlib
 import os
@@ -27,9 +25,7 @@ c, ref = pkg.synthetic.candidates(n, K, R, t, seed=0)
 dev = torch.device("cuda:0")
 ctx = pkg.MvsContext(rgb, K, R, t, device=0)
 mode = os.environ.get("MODE", "lib")
-ctx2 = pkg.MvsContext(rgb, K, R, t, device=0) if mode in ("ctx", "gate") else ctx
-if mode == "gate":
-    ctx.pair_scorers(ctx2)
+ctx2 = pkg.MvsContext(rgb, K, R, t, device=0) if mode == "ctx" else ctx
 tc, tr = torch.from_numpy(c).to(dev), torch.from_numpy(ref).to(dev)
 xys = [torch.empty((n, 2), dtype=torch.float64, device=dev) for _ in range(2)]
 recs = [torch.empty((n, 2), dtype=torch.int64, device=dev) for _ in range(2)]
