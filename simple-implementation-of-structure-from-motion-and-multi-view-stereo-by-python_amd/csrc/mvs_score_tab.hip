@@ -39,10 +39,16 @@ template <int WID, bool DTAB>
 __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const MomentsDev mt) {
     constexpr int NB = 2 * WID + 1, NPX = NB * NB;
     // LDS column c holds image column x0 - 8 + c: 48 bytes cover the block's
-    // 32 columns and both window halos (WID <= 5 < 8)
-    constexpr int ROWS = kMomH + 2 * WID, CP = 48, CW = CP / 4;
-    __shared__ __attribute__((aligned(16))) uint32_t g4[kMomV][ROWS][CW];
-    __shared__ uint32_t hs[kMomV][ROWS][kMomW];
+    // 32 columns and both window halos (WID <= 5 < 8).  Pitches chosen for
+    // the LDS banks: a gray row of 13 dwords (the horizontal pass's lanes walk
+    // consecutive rows: odd stride), the sums' row of 33 words (same), and a
+    // view stride VS = 4 (mod 64) -- the vertical pass's lanes are 16 views x
+    // 4 columns of one row, 64 distinct banks (rows of 32 words and no view
+    // pad put the 16 views of a column in one bank: 16-way conflicts)
+    constexpr int ROWS = kMomH + 2 * WID, CP = 48, CW = CP / 4, GP = CW + 1, HP = kMomW + 1;
+    constexpr int VS = ROWS * HP + (((4 - ROWS * HP) % 64) + 64) % 64;
+    __shared__ __attribute__((aligned(16))) uint32_t g4[kMomV][ROWS][GP];
+    __shared__ uint32_t hs[kMomV * VS];
     const int x0 = blockIdx.x * kMomW, y0 = blockIdx.y * kMomH, v0 = blockIdx.z * kMomV;
     const int tid = threadIdx.x;
     const int nv = min(kMomV, sc.V - v0);
@@ -50,31 +56,44 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
     // rows (signed s = g - 128; 8 pad bytes left of column 0 and >= 24 right
     // of W-1, so [x0 - 8, x0 + 40) is inside the row's pitch or, for the last
     // columns, the next row's start / the buffer's 64-byte tail, never used
-    // by a valid window); rows outside the image clamped; views past V zero
-    for (int k = tid; k < kMomV * ROWS * CW; k += 256) {
+    // by a valid window); rows outside the image clamped; views past V zero.
+    // Every load of the thread in flight at once, then the LDS writes (a
+    // load-then-write loop waited for each load in turn)
+    constexpr int NLD = kMomV * ROWS * CW, PER = (NLD + 255) / 256;
+    uint32_t buf[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int k = tid + 256 * j;
         const int vi = k / (ROWS * CW), rc = k - vi * (ROWS * CW), r = rc / CW, c = rc - r * CW;
         const int y = min(max(y0 - WID + r, 0), sc.H - 1);
         uint32_t wv = 0u;
-        if (vi < nv)
-            wv = *(const uint32_t*)(sc.gv + ((int64_t)(v0 + vi) * sc.H + y) * sc.Wp + x0 - 8 + 4 * c) ^ 0x80808080u;
-        g4[vi][r][c] = wv;
+        if (k < NLD && vi < nv)
+            wv = *(const uint32_t*)(sc.gv + ((int64_t)(v0 + vi) * sc.H + y) * sc.Wp + x0 - 8 + 4 * c);
+        buf[j] = wv;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int k = tid + 256 * j;
+        const int vi = k / (ROWS * CW), rc = k - vi * (ROWS * CW), r = rc / CW, c = rc - r * CW;
+        if (k < NLD) g4[vi][r][c] = vi < nv ? buf[j] ^ 0x80808080u : 0u;
     }
     __syncthreads();
     for (int k = tid; k < kMomV * ROWS; k += 256) {
         const int vi = k / ROWS, r = k - vi * ROWS;
         const uint8_t* row = (const uint8_t*)g4[vi][r] + 8 - WID;   // image column x0 - WID
+        uint32_t* hrow = hs + vi * VS + r * HP;
         uint32_t S = 0, Q = 0;
 #pragma unroll
         for (int c = 0; c < NB; ++c) {
             S += row[c];
             Q += (uint32_t)row[c] * row[c];
         }
-        hs[vi][r][0] = (Q << 12) | S;
+        hrow[0] = (Q << 12) | S;
         for (int x = 1; x < kMomW; ++x) {
             const uint32_t a = row[x - 1], b = row[x + NB - 1];
             S += b - a;
             Q += b * b - a * a;
-            hs[vi][r][x] = (Q << 12) | S;
+            hrow[x] = (Q << 12) | S;
         }
     }
     __syncthreads();
@@ -83,16 +102,17 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
         const int vi = k & (kMomV - 1), xl = k >> 4;
         const int x = x0 + xl;
         if (x < x_lo || x > x_hi) continue;
+        const uint32_t* hcol = hs + vi * VS + xl;
         int S = 0, Q = 0;
 #pragma unroll
         for (int r = 0; r < NB; ++r) {
-            const uint32_t h = hs[vi][r][xl];
+            const uint32_t h = hcol[r * HP];
             S += (int)(h & 0xfffu);
             Q += (int)(h >> 12);
         }
         for (int yl = 0; yl < kMomH; ++yl) {
             if (yl > 0) {
-                const uint32_t a = hs[vi][yl - 1][xl], b = hs[vi][yl + NB - 1][xl];
+                const uint32_t a = hcol[(yl - 1) * HP], b = hcol[(yl + NB - 1) * HP];
                 S += (int)(b & 0xfffu) - (int)(a & 0xfffu);
                 Q += (int)(b >> 12) - (int)(a >> 12);
             }
