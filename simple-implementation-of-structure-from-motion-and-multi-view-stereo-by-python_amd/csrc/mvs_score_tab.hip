@@ -24,9 +24,9 @@ namespace {
 // k_moments: S_b and w_b of every (pixel, view) with a valid window
 // (getDescFeatures' bounds, HarrisFeatures.py:128), 32 columns x 16 rows x 16
 // views per workgroup.  The gray bytes of the block's views and rows land in
-// LDS; per (view, row) the horizontal window sums (S = sum g, Q = sum g^2 of
-// the unsigned g, packed Q << 12 | S) by a running prefix; per (view, column)
-// the vertical sums slide down the 16 rows.  The same arithmetic as the
+// LDS; per (view, column) a thread forms every row's horizontal window sums
+// (S = sum g, Q = sum g^2 of the unsigned g, packed Q << 12 | S) by byte dot
+// products in registers, and the vertical sums slide down the 16 rows.  The same arithmetic as the
 // in-kernel moments of k_score_mma (the tables are bit-identical to them):
 // D = n Q - S^2 (exact int32), w = v_rsq_f64(D) + one Newton step (a constant
 // window: D = 0, inf, then nan), S_b = S - 128 n; and a bit per (pixel, view)
@@ -39,16 +39,13 @@ template <int WID, bool DTAB>
 __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const MomentsDev mt) {
     constexpr int NB = 2 * WID + 1, NPX = NB * NB;
     // LDS column c holds image column x0 - 8 + c: 48 bytes cover the block's
-    // 32 columns and both window halos (WID <= 5 < 8).  Pitches chosen for
-    // the LDS banks: a gray row of 13 dwords (the horizontal pass's lanes walk
-    // consecutive rows: odd stride), the sums' row of 33 words (same), and a
-    // view stride VS = 4 (mod 64) -- the vertical pass's lanes are 16 views x
-    // 4 columns of one row, 64 distinct banks (rows of 32 words and no view
-    // pad put the 16 views of a column in one bank: 16-way conflicts)
-    constexpr int ROWS = kMomH + 2 * WID, CP = 48, CW = CP / 4, GP = CW + 1, HP = kMomW + 1;
-    constexpr int VS = ROWS * HP + (((4 - ROWS * HP) % 64) + 64) % 64;
+    // 32 columns and both window halos (WID <= 5 < 8); rows of 13 dwords
+    // (the lanes of a read are 16 views x 4 columns: a view stride of 13 ROWS
+    // dwords spreads them over the banks).  The only LDS array: 21 KB at
+    // WID 5, so up to 7 workgroups share a CU (a 58 KB table of the
+    // horizontal sums held it to 2: 73 us per dinoRing scene)
+    constexpr int ROWS = kMomH + 2 * WID, CP = 48, CW = CP / 4, GP = CW + 1;
     __shared__ __attribute__((aligned(16))) uint32_t g4[kMomV][ROWS][GP];
-    __shared__ uint32_t hs[kMomV * VS];
     const int x0 = blockIdx.x * kMomW, y0 = blockIdx.y * kMomH, v0 = blockIdx.z * kMomV;
     const int tid = threadIdx.x;
     const int nv = min(kMomV, sc.V - v0);
@@ -78,41 +75,45 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
         if (k < NLD) g4[vi][r][c] = vi < nv ? buf[j] ^ 0x80808080u : 0u;
     }
     __syncthreads();
-    for (int k = tid; k < kMomV * ROWS; k += 256) {
-        const int vi = k / ROWS, r = k - vi * ROWS;
-        const uint8_t* row = (const uint8_t*)g4[vi][r] + 8 - WID;   // image column x0 - WID
-        uint32_t* hrow = hs + vi * VS + r * HP;
-        uint32_t S = 0, Q = 0;
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-            S += row[c];
-            Q += (uint32_t)row[c] * row[c];
-        }
-        hrow[0] = (Q << 12) | S;
-        for (int x = 1; x < kMomW; ++x) {
-            const uint32_t a = row[x - 1], b = row[x + NB - 1];
-            S += b - a;
-            Q += b * b - a * a;
-            hrow[x] = (Q << 12) | S;
-        }
-    }
-    __syncthreads();
     const int x_lo = WID + 1, x_hi = sc.W - WID - 2, y_lo = WID, y_hi = sc.H - WID - 2;   // valid centres
+    // the window's NB bytes of a row: NF whole aligned dwords and NR bytes
+    constexpr int NF = NB / 4, NR = NB % 4, ND = NF + (NR ? 1 : 0);
     for (int k = tid; k < kMomV * kMomW; k += 256) {
         const int vi = k & (kMomV - 1), xl = k >> 4;
         const int x = x0 + xl;
         if (x < x_lo || x > x_hi) continue;
-        const uint32_t* hcol = hs + vi * VS + xl;
+        // per row r of the block: the horizontal window sums S = sum g and
+        // Q = sum g^2 of the unsigned bytes (exact integers, packed Q << 12 |
+        // S) by byte dot products over the window's bytes, realigned from
+        // the row's dwords; every row's reads in flight together
+        const int b0 = 8 - WID + xl, sh = b0 & 3, d0 = b0 >> 2;   // image column x - WID
+        uint32_t hp[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const uint32_t* gr = &g4[vi][r][d0];
+            uint32_t wd[ND + 1];
+#pragma unroll
+            for (int j = 0; j <= ND; ++j) wd[j] = gr[j];
+            uint32_t S = 0u, Q = 0u;
+#pragma unroll
+            for (int j = 0; j < ND; ++j) {
+                uint32_t a = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], (uint32_t)sh);
+                if (j == NF) a &= (1u << (8 * NR)) - 1u;
+                S = __builtin_amdgcn_udot4(a, 0x01010101u, S, false);
+                Q = __builtin_amdgcn_udot4(a, a, Q, false);
+            }
+            hp[r] = (Q << 12) | S;
+        }
         int S = 0, Q = 0;
 #pragma unroll
         for (int r = 0; r < NB; ++r) {
-            const uint32_t h = hcol[r * HP];
-            S += (int)(h & 0xfffu);
-            Q += (int)(h >> 12);
+            S += (int)(hp[r] & 0xfffu);
+            Q += (int)(hp[r] >> 12);
         }
+#pragma unroll
         for (int yl = 0; yl < kMomH; ++yl) {
             if (yl > 0) {
-                const uint32_t a = hcol[(yl - 1) * HP], b = hcol[(yl + NB - 1) * HP];
+                const uint32_t a = hp[yl - 1], b = hp[yl + NB - 1];
                 S += (int)(b & 0xfffu) - (int)(a & 0xfffu);
                 Q += (int)(b >> 12) - (int)(a >> 12);
             }
