@@ -18,7 +18,7 @@ acc = collections.defaultdict(lambda: collections.defaultdict(lambda: collection
 for f in sorted(glob.glob(os.path.join(sys.argv[1], "p*", "run_counter_collection.csv"))):
     for row in csv.DictReader(open(f)):
         m = re.search(r"(k_\w+)", row["Kernel_Name"])
-        if m and m.group(1) in ("k_bin", "k_score_tab", "k_score_fix", "k_acc_pack"):
+        if m and m.group(1) in ("k_bin", "k_score_tab", "k_score_fix", "k_acc_pack", "k_moments", "k_build_scene"):
             acc[m.group(1)][row["Counter_Name"]][(f, row["Dispatch_Id"])] += float(row["Counter_Value"])
 for k, d in acc.items():
     print(k)
