@@ -78,8 +78,11 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
     const int x_lo = WID + 1, x_hi = sc.W - WID - 2, y_lo = WID, y_hi = sc.H - WID - 2;   // valid centres
     // the window's NB bytes of a row: NF whole aligned dwords and NR bytes
     constexpr int NF = NB / 4, NR = NB % 4, ND = NF + (NR ? 1 : 0);
-    for (int k = tid; k < kMomV * kMomW; k += 256) {
-        const int vi = k & (kMomV - 1), xl = k >> 4;
+    // a task = (view, column, half of the block's rows): 8 output rows from
+    // 8 + 2 WID rows of horizontal sums (fewer live registers than all 16)
+    constexpr int OH = kMomH / 2, RH = OH + 2 * WID;
+    for (int k = tid; k < kMomV * kMomW * 2; k += 256) {
+        const int vi = k & (kMomV - 1), xl = (k >> 4) & (kMomW - 1), rb = (k >> 9) * OH;
         const int x = x0 + xl;
         if (x < x_lo || x > x_hi) continue;
         // per row r of the block: the horizontal window sums S = sum g and
@@ -87,10 +90,10 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
         // S) by byte dot products over the window's bytes, realigned from
         // the row's dwords; every row's reads in flight together
         const int b0 = 8 - WID + xl, sh = b0 & 3, d0 = b0 >> 2;   // image column x - WID
-        uint32_t hp[ROWS];
+        uint32_t hp[RH];
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-            const uint32_t* gr = &g4[vi][r][d0];
+        for (int r = 0; r < RH; ++r) {
+            const uint32_t* gr = &g4[vi][rb + r][d0];
             uint32_t wd[ND + 1];
 #pragma unroll
             for (int j = 0; j <= ND; ++j) wd[j] = gr[j];
@@ -111,13 +114,13 @@ __global__ __launch_bounds__(256) void k_moments(const SceneDev sc, const Moment
             Q += (int)(hp[r] >> 12);
         }
 #pragma unroll
-        for (int yl = 0; yl < kMomH; ++yl) {
+        for (int yl = 0; yl < OH; ++yl) {
             if (yl > 0) {
                 const uint32_t a = hp[yl - 1], b = hp[yl + NB - 1];
                 S += (int)(b & 0xfffu) - (int)(a & 0xfffu);
                 Q += (int)(b >> 12) - (int)(a >> 12);
             }
-            const int y = y0 + yl;
+            const int y = y0 + rb + yl;
             if (y < y_lo || y > y_hi) continue;
             const int64_t o = ((int64_t)y * sc.W + x) * mt.VP + v0 + vi;
             // the constant windows (D = 0) of the pixel's 16 views as one
